@@ -1,0 +1,299 @@
+"""CPU oracle for the formation env hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` may
+import this module.  It is the checker, never the thing measured or shipped: the product path
+(``marl-distributedformation_amd``) runs the HIP library and fails loudly without it.
+
+Two restatements of the same algorithm (reference ``simulate.py:70-236`` and
+``vectorized_env.py:22-82``, global torch CPU MT19937 resets ``simulate.py:120-147``):
+
+* :class:`COracleEnv` -- ctypes wrapper of ``oracle/fenv_oracle.c`` (scalar, bit-exact fp32).
+* :class:`NumpyOracleEnv` -- vectorised numpy restatement, bit-exact too (fma emulated exactly).
+
+Both are pinned against ``tests/golden/*.npz`` (fixtures produced by importing the reference
+itself in the build container, ``tests/golden/gen_golden.py``).
+
+:func:`synth_actions` is the deterministic synthetic action stream every parity test and the
+golden generator share (splitmix64 hash of (seed, step, element) -> U(-amp, amp) in fp32).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+W, H = 400.0, 600.0
+MAX_STEPS = 1000
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+# ----------------------------------------------------------------------------- actions
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_actions(seed: int, step: int, num_agents: int, amp: float = 1.0) -> np.ndarray:
+    """Deterministic U(-amp, amp) fp32 actions [num_agents, 2] for (seed, step)."""
+    with np.errstate(over="ignore"):
+        base = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15)
+                + np.uint64(step) * np.uint64(0xD1B54A32D192ED03))
+        idx = np.arange(2 * num_agents, dtype=np.uint64)
+        z = _splitmix64(base + idx)
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
+    a = (u * np.float32(2.0) - np.float32(1.0)) * np.float32(amp)
+    return a.astype(np.float32).reshape(num_agents, 2)
+
+
+# ----------------------------------------------------------------------------- MT19937
+def mt_raw(seed: int, n: int, skip: int = 0) -> np.ndarray:
+    """Raw 32-bit MT19937 outputs after init_genrand(seed) (== torch.manual_seed stream)."""
+    bg = np.random.MT19937()
+    bg._legacy_seeding(int(seed) & 0xFFFFFFFF)
+    if skip:
+        bg.random_raw(skip)
+    return bg.random_raw(n).astype(np.uint32)
+
+
+def torch_rand_from_raw(raw: np.ndarray) -> np.ndarray:
+    return (raw & np.uint32(0xFFFFFF)).astype(np.float32) * np.float32(2.0 ** -24)
+
+
+# ----------------------------------------------------------------------------- exact fmaf
+def fmaf(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """Correctly rounded fp32 fma(a, b, c) for fp32 arrays (one rounding, like v_fma_f32)."""
+    a64, b64, c64 = (np.asarray(v, np.float32).astype(np.float64) for v in (a, b, c))
+    p = a64 * b64                      # exact: 24x24-bit product fits in 53 bits
+    s = p + c64
+    bb = s - p                          # TwoSum: p + c64 == s + e exactly
+    e = (p - (s - bb)) + (c64 - bb)
+    r = s.astype(np.float32)
+    r64 = r.astype(np.float64)
+    inexact = (r64 != s) & (e != 0)
+    if np.any(inexact):
+        toward = np.where(s > r64, np.float32(np.inf), np.float32(-np.inf))
+        n = np.nextafter(r, toward.astype(np.float32))
+        mid = (r64 + n.astype(np.float64)) * 0.5
+        tie = inexact & (s == mid)
+        # at an exact double tie the true value lies on e's side
+        go_n = tie & ((e > 0) == (n.astype(np.float64) > r64))
+        r = np.where(go_n, n, r)
+    return r.astype(np.float32)
+
+
+def norm2(x: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """torch CPU linalg.norm(dim=1) of 2-vectors == sqrtf(fmaf(y, y, x*x))."""
+    x = np.asarray(x, np.float32)
+    y = np.asarray(y, np.float32)
+    return np.sqrt(fmaf(y, y, x * x)).astype(np.float32)
+
+
+def desired_neighbor_dist(n: int) -> np.float32:
+    """simulate.py:26, rounded to fp32 when it meets the fp32 tensor (simulate.py:202-203)."""
+    return np.float32(2 * 60 * np.sin(np.pi / n))
+
+
+# ----------------------------------------------------------------------------- numpy env
+class NumpyOracleEnv:
+    """Vectorised restatement of FormationEnv (vectorized_env.py:16-82) over [F, N] arrays."""
+
+    def __init__(self, num_formation: int, num_agents: int, goal_in_obs: bool = True,
+                 seed: int = 0, share: float = 0.25, max_steps: int = MAX_STEPS):
+        self.F, self.N = int(num_formation), int(num_agents)
+        self.goal_in_obs = bool(goal_in_obs)
+        self.D = 8 if goal_in_obs else 6
+        self.max_steps = int(max_steps)
+        self.c_self = np.float32(1.0 - 2 * share)
+        self.c_nb = np.float32(share)
+        self.d_nb = desired_neighbor_dist(self.N)
+        self._bg = np.random.MT19937()
+        self._bg._legacy_seeding(int(seed) & 0xFFFFFFFF)
+        self.p = np.zeros((self.F, self.N, 2), np.float32)
+        self.g = np.zeros((self.F, 2), np.float32)
+        self.t = np.zeros(self.F, np.int32)
+        self._reset_formations(np.arange(self.F))      # ctor draw set (simulate.py:61)
+
+    # simulate.py:120-147, drawn in formation order
+    def _reset_formations(self, idx: np.ndarray) -> None:
+        k = len(idx)
+        if k == 0:
+            return
+        per = 2 * self.N + 2
+        u = torch_rand_from_raw(self._bg.random_raw(k * per).astype(np.uint32)).reshape(k, per)
+        ua = u[:, :2 * self.N].reshape(k, self.N, 2)
+        self.p[idx, :, 0] = ua[:, :, 0] * np.float32(400)
+        self.p[idx, :, 1] = ua[:, :, 1] * np.float32(100)
+        self.g[idx, 0] = u[:, -2] * np.float32(280) + np.float32(60)
+        self.g[idx, 1] = u[:, -1] * np.float32(480) + np.float32(60)
+        self.t[idx] = 0
+
+    def observe(self) -> np.ndarray:
+        n = self.p / np.array([W, H], np.float32)
+        prev = np.roll(n, 1, axis=1)
+        nxt = np.roll(n, -1, axis=1)
+        parts = [n, prev - n, nxt - n]
+        if self.goal_in_obs:
+            parts.append((self.g[:, None, :] - self.p) / np.array([W, H], np.float32))
+        return np.concatenate(parts, axis=2).reshape(self.F * self.N, self.D).astype(np.float32)
+
+    def reset(self) -> np.ndarray:
+        self._reset_formations(np.arange(self.F))
+        return self.observe()
+
+    def step(self, actions: np.ndarray):
+        a = np.asarray(actions, np.float32).reshape(self.F, self.N, 2)
+        p = self.p + np.float32(10) * a
+        oob = ((p[..., 0] <= 0) | (p[..., 1] <= 0) | (p[..., 0] >= np.float32(W))
+               | (p[..., 1] >= np.float32(H)))
+        p[..., 0] = np.where(p[..., 0] < 0, np.float32(0),
+                             np.where(p[..., 0] > np.float32(W), np.float32(W), p[..., 0]))
+        p[..., 1] = np.where(p[..., 1] < 0, np.float32(0),
+                             np.where(p[..., 1] > np.float32(H), np.float32(H), p[..., 1]))
+        self.p = p.astype(np.float32)
+        dg = norm2(p[..., 0] - self.g[:, None, 0], p[..., 1] - self.g[:, None, 1])
+        ctg = np.where(dg < np.float32(100), np.float32(10), np.float32(0))
+        rd = np.float32(-0.1) * dg
+        pr = np.roll(p, -1, axis=1)
+        pl = np.roll(p, 1, axis=1)
+        dr = norm2(p[..., 0] - pr[..., 0], p[..., 1] - pr[..., 1]) - self.d_nb
+        dl = norm2(p[..., 0] - pl[..., 0], p[..., 1] - pl[..., 1]) - self.d_nb
+        rr = np.float32(-0.01) * np.where(dr < 0, dr * dr, dr)
+        rl = np.float32(-0.01) * np.where(dl < 0, dl * dl, dl)
+        ind = ((rd + ctg) + rr) + rl
+        ind = ind + (np.where(oob, np.float32(-100), np.float32(-0.0)) + np.float32(-0.0))
+        rew = (self.c_self * ind
+               + self.c_nb * (np.roll(ind, 1, axis=1) + np.roll(ind, -1, axis=1)))
+        done_f = self.t > self.max_steps
+        self.t = self.t + 1
+        self._reset_formations(np.nonzero(done_f)[0])
+        done = np.repeat(done_f, self.N)
+        return (self.observe(), rew.astype(np.float32).reshape(-1), done,
+                None)
+
+    def metrics(self, rew: np.ndarray | None = None) -> np.ndarray:
+        """Per-formation [avg_dist_to_goal, mean right-neighbour dist, its unbiased std,
+        mean reward] (simulate.py:238-254, vectorized_env.py:80-81), float64."""
+        p = self.p.astype(np.float32)
+        dg = norm2(p[..., 0] - self.g[:, None, 0], p[..., 1] - self.g[:, None, 1]).astype(np.float64)
+        pr = np.roll(p, -1, axis=1)
+        dr = norm2(p[..., 0] - pr[..., 0], p[..., 1] - pr[..., 1]).astype(np.float64)
+        out = np.zeros((self.F, 4))
+        out[:, 0] = dg.mean(1)
+        out[:, 1] = dr.mean(1)
+        out[:, 2] = dr.std(1, ddof=1) if self.N > 1 else np.nan
+        out[:, 3] = 0.0 if rew is None else np.asarray(rew, np.float64).reshape(self.F, self.N).mean(1)
+        return out
+
+    def get_state(self):
+        return (self.p[..., 0].reshape(-1).copy(), self.p[..., 1].reshape(-1).copy(),
+                self.g[:, 0].copy(), self.g[:, 1].copy(), self.t.copy())
+
+
+# ----------------------------------------------------------------------------- C oracle
+_lib = None
+
+
+def load_lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        lib.orc_env_create.restype = P
+        lib.orc_env_create.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_double, ctypes.c_int32, ctypes.c_uint32]
+        lib.orc_env_destroy.argtypes = [P]
+        lib.orc_env_reset.argtypes = [P, P]
+        lib.orc_env_observe.argtypes = [P, P]
+        lib.orc_env_step.argtypes = [P, P, P, P, P]
+        lib.orc_env_metrics.argtypes = [P, P, P]
+        lib.orc_env_get_state.argtypes = [P, P, P, P, P, P]
+        lib.orc_env_set_state.argtypes = [P, P, P, P, P, P]
+        lib.orc_env_d_nb.argtypes = [P]
+        lib.orc_env_d_nb.restype = ctypes.c_float
+        lib.orc_mt_raw.argtypes = [ctypes.c_uint32, ctypes.c_uint64, P, ctypes.c_int64]
+        _lib = lib
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class COracleEnv:
+    """ctypes wrapper of fenv_oracle.c with the FormationEnv surface (numpy in/out)."""
+
+    def __init__(self, num_formation: int, num_agents: int, goal_in_obs: bool = True,
+                 seed: int = 0, share: float = 0.25, max_steps: int = MAX_STEPS):
+        self.lib = load_lib()
+        self.F, self.N = int(num_formation), int(num_agents)
+        self.D = 8 if goal_in_obs else 6
+        self.A = self.F * self.N
+        self.h = self.lib.orc_env_create(self.F, self.N, int(bool(goal_in_obs)), float(share),
+                                         int(max_steps), int(seed) & 0xFFFFFFFF)
+        self.obs = np.zeros((self.A, self.D), np.float32)
+        self.rew = np.zeros(self.A, np.float32)
+        self.done = np.zeros(self.A, np.bool_)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.lib.orc_env_destroy(h)
+            self.h = None
+
+    def reset(self) -> np.ndarray:
+        self.lib.orc_env_reset(self.h, _ptr(self.obs))
+        return self.obs.copy()
+
+    def observe(self) -> np.ndarray:
+        self.lib.orc_env_observe(self.h, _ptr(self.obs))
+        return self.obs.copy()
+
+    def step(self, actions: np.ndarray):
+        a = np.ascontiguousarray(actions, np.float32).reshape(self.A, 2)
+        self.lib.orc_env_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.rew), _ptr(self.done))
+        return self.obs.copy(), self.rew.copy(), self.done.copy(), None
+
+    def step_inplace(self, actions: np.ndarray) -> None:
+        """Same as step() without the copies (for timing the CPU baseline)."""
+        self.lib.orc_env_step(self.h, _ptr(actions), _ptr(self.obs), _ptr(self.rew),
+                              _ptr(self.done))
+
+    def metrics(self, rew: np.ndarray | None = None) -> np.ndarray:
+        out = np.zeros((self.F, 4), np.float64)
+        r = None if rew is None else np.ascontiguousarray(rew, np.float32)
+        self.lib.orc_env_metrics(self.h, None if r is None else _ptr(r), _ptr(out))
+        return out
+
+    def get_state(self):
+        px = np.zeros(self.A, np.float32)
+        py = np.zeros(self.A, np.float32)
+        gx = np.zeros(self.F, np.float32)
+        gy = np.zeros(self.F, np.float32)
+        t = np.zeros(self.F, np.int32)
+        self.lib.orc_env_get_state(self.h, _ptr(px), _ptr(py), _ptr(gx), _ptr(gy), _ptr(t))
+        return px, py, gx, gy, t
+
+    def set_state(self, px, py, gx, gy, t) -> None:
+        arrs = [np.ascontiguousarray(v, np.float32) for v in (px, py, gx, gy)]
+        tt = np.ascontiguousarray(t, np.int32)
+        self.lib.orc_env_set_state(self.h, *[_ptr(v) for v in arrs], _ptr(tt))
+
+    @property
+    def d_nb(self) -> float:
+        return float(self.lib.orc_env_d_nb(self.h))
+
+
+def c_mt_raw(seed: int, n: int, skip: int = 0) -> np.ndarray:
+    out = np.zeros(n, np.uint32)
+    load_lib().orc_mt_raw(int(seed) & 0xFFFFFFFF, int(skip), _ptr(out), int(n))
+    return out
