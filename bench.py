@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: synthetic random-action rollouts of the formation env on MI355X.
+
+Metric (BASELINE.json): agent-steps/sec (whole node) at 5 agents/formation, and the step
+kernel's fraction of the HBM roofline.  Workload: BASELINE config 3 -- 1,048,576 formations x 5
+agents (5,242,880 agents), sharded contiguously over the ranks (strong scaling: the same batch
+on 1, 2, 4 or 8 GPUs).  A "step" is one env step of every agent; steps run as fused rollouts of
+`--chunk` steps per launch (SB3's n_steps=10 rollout, vectorized_env.py:128) writing obs /
+reward / done for every step into a device rollout buffer, with the actions read from HBM
+(inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
+over RCCL once per rollout on a side stream.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-steps/sec (whole node) at 5 agents/formation; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def rollout_bytes_per_launch(A: int, N: int, D: int, T: int) -> float:
+    """Algorithmic HBM bytes of one fenv_rollout launch:
+    per agent-step: action 8 + obs 4D + reward 4 + done 1; per agent-launch: position read +
+    write 16, formation goal 8 + steps_since_reset 4+4 + episode 4 read, per formation."""
+    per_step = 8 + 4 * D + 4 + 1
+    per_launch = 16 + (8 + 8 + 4) / N
+    return A * (T * per_step + per_launch)
+
+
+def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
+    """Time the bit-exact C port of the reference env (oracle/, 1 thread) on a bounded sample
+    of the same workload (random U(-1,1) actions, 5 agents/formation)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import COracleEnv
+    F = 65536
+    env = COracleEnv(F, N, D == 8, 0)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = [rng.uniform(-1, 1, (F * N, 2)).astype(np.float32) for _ in range(4)]
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        env.step_inplace(acts[steps % 4])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": F * N * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{F} formations x {N} agents, {steps} env steps ({el:.1f} s), "
+                      f"oracle/fenv_oracle.c (bit-exact C port of simulate.py/vectorized_env.py)"
+                      f", 1 thread of {os.cpu_count()} host CPUs"}
+
+
+def load_pmc_traffic(workload: str):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    try:
+        d = json.load(open(p))
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch"), p
+    except Exception:
+        pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--formations", type=int, default=1 << 20)
+    ap.add_argument("--agents", type=int, default=5)
+    ap.add_argument("--chunk", type=int, default=10)
+    ap.add_argument("--reset-mode", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--no-goal", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import pkgload
+    pkg = pkgload.load()
+    from importlib import import_module
+    venv = import_module(pkg.__name__ + ".vectorized_env")
+    pdist = import_module(pkg.__name__ + ".distributed")
+
+    rank, world, local = pdist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    N, T = args.agents, args.chunk
+    D = 6 if args.no_goal else 8
+    first, F = pdist.shard_range(args.formations, rank, world)
+    cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": not args.no_goal}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode=args.reset_mode,
+                            first_formation=first, total_formations=args.formations)
+    A = F * N
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    acts = [(torch.rand((T, A, 2), device=dev, generator=g) * 2 - 1) for _ in range(2)]
+    obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
+    rew = torch.empty((T, A), dtype=torch.float32, device=dev)
+    done = torch.empty((T, A), dtype=torch.bool, device=dev)
+    partial = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=dev)
+    red = torch.zeros(2, dtype=torch.float64, device=dev)
+    stats = pdist.StatsReducer(2, dev)
+    env.reset_tensor()
+
+    def chunk(k, ev=None):
+        if ev is not None:
+            ev[0].record()
+        env.rollout(acts[k % 2], obs, rew, done, partial=None if args.no_stats else partial)
+        if ev is not None:
+            ev[1].record()
+        if not args.no_stats:
+            env.reduce_partials(partial, red)
+            stats.submit(red)
+
+    warm_chunks = max(1, -(-args.warmup // T))
+    n_chunks = max(1, -(-args.steps // T))
+    steps = n_chunks * T
+    for k in range(warm_chunks):
+        chunk(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_chunks)]
+    t0 = time.perf_counter()
+    for k in range(n_chunks):
+        chunk(k, evs[k])
+    if not args.no_stats:
+        tot = stats.result()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    elapsed = pdist.max_over_ranks(elapsed, dev)
+    kern_avg_ms = pdist.max_over_ranks(kern_avg_ms, dev)
+
+    total_agents = args.formations * N
+    value = total_agents * steps / elapsed
+    bytes_launch = rollout_bytes_per_launch(A, N, D, T)
+    achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
+    workload = (f"config3: {args.formations} formations x {N} agents, fused {T}-step "
+                f"rollouts, {args.reset_mode} resets")
+    traffic, tsrc = load_pmc_traffic(workload if world == 1 else "")
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warm_chunks * T,
+            "ms_per_step": elapsed * 1e3 / steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: U(-1,1) fp32 actions resident in HBM, random-init formations",
+            "config": {"workload": workload, "formations": args.formations,
+                       "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
+                       "formations_per_gpu": F, "reset_mode": args.reset_mode,
+                       "parallelism": f"formation-shard dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": "k_rollout_wave (fenv_rollout)",
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "avg_kernel_ms": kern_avg_ms, "launches": n_chunks},
+        }
+        if not args.no_stats:
+            t = tot.cpu().tolist()
+            out["episode_stats"] = {"mean_reward": t[0] / (total_agents * T),
+                                    "agent_dones_last_rollout": t[1]}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

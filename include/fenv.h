@@ -1,0 +1,143 @@
+/*
+ * fenv.h -- C ABI of the MI355X (gfx950) batched formation env + policy rollout library
+ * (libfenv.so, built from marl-distributedformation_amd/csrc/).
+ *
+ * The reference exposes this hot path as the stable-baselines3 VecEnv Python object
+ * FormationEnv (/root/reference/vectorized_env.py:16-109) over per-formation
+ * FormationSimulator objects (/root/reference/simulate.py:7-254), plus SB3's MlpPolicy
+ * forward (call site vectorized_env.py:126).  Each entry point below replaces one piece of that
+ * interface; the Python mirror (marl-distributedformation_amd/vectorized_env.py) keeps the
+ * reference's method names and binds these symbols with ctypes.
+ *
+ * Conventions
+ *  - Plain C types only.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *  - Every buffer argument named obs/act/rew/done/out/params/... is a DEVICE pointer owned
+ *    by the caller unless the name ends in `_host`.  Env state is owned by the handle.
+ *  - Layouts: act [T][A][2] f32, obs [T][A][D] f32 (D = 8 if goal_in_obs else 6),
+ *    rew [T][A] f32, done [T][A] u8 (0/1), with A = num_formation * num_agents and agents of
+ *    formation f at rows f*N .. f*N+N-1 (vectorized_env.py:72-79 ordering).
+ *  - All calls are asynchronous on `stream` unless stated; none throws.  Return 0 on success,
+ *    a negative FENV_E* code on failure; fenv_last_error() gives a thread-local message.
+ *  - One handle is used from one host thread at a time.
+ */
+#ifndef FENV_H
+#define FENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fenv fenv_t;
+
+enum {
+    FENV_OK = 0,
+    FENV_EINVAL = -1,  /* bad argument (shape/size/pointer/mode) */
+    FENV_EHIP = -2,    /* HIP runtime error (no device, launch failure, ...) */
+    FENV_ESTATE = -3,  /* operation not valid in the handle's current state */
+    FENV_ENOMEM = -4
+};
+
+/* Reset RNG modes. */
+enum {
+    /* Bit-for-bit the reference: one global MT19937 stream seeded like torch.manual_seed(seed),
+       drawn on the host in formation order (simulate.py:125,133,140) and staged to HBM. */
+    FENV_RESET_MT19937 = 0,
+    /* Throughput mode: counter-based Philox4x32-10 keyed by (seed, global formation, episode),
+       drawn inside the kernels.  Same distributions, not the reference's stream. */
+    FENV_RESET_PHILOX = 1
+};
+
+/* Replaces FormationEnv.__init__ (vectorized_env.py:22-50) for the formations
+ * [first_formation, first_formation + num_formation) of a batch of total_formations
+ * (sharding; pass 0 and num_formation for an unsharded env).  Like the reference ctor it
+ * consumes the first reset draw set (simulate.py:61).  share_reward_ratio is the simulator's
+ * (simulate.py:11; the reference env never forwards its cfg key, so pass 0.25 for parity).
+ * Formation sizes: 1 <= num_agents <= 1024. */
+int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num_agents,
+                int32_t goal_in_obs, double share_reward_ratio, int32_t max_steps, uint32_t seed,
+                int32_t reset_mode, int64_t first_formation, int64_t total_formations);
+
+int fenv_destroy(fenv_t *env);
+
+/* out_host[0..7] = {num_formation, num_agents, obs_dim, num_agents_total(A), steps_since_reset
+ * (common value, -1 if formations differ), reset_mode, first_formation, total_formations}. */
+int fenv_info(const fenv_t *env, int64_t *out_host);
+
+/* Replaces FormationEnv.reset (vectorized_env.py:52-55): new draw set for every formation, then
+ * compute_observations (:57-66) into obs [A][D] (obs may be NULL). */
+int fenv_reset(fenv_t *env, float *obs, void *stream);
+
+/* compute_observations (vectorized_env.py:57-66 / simulate.py:150-174) of the current state. */
+int fenv_observe(fenv_t *env, float *obs, void *stream);
+
+/* Replaces FormationEnv.step (vectorized_env.py:68-82) -> FormationSimulator.step
+ * (simulate.py:70-118) for every formation: act [A][2] in the SB3 action space (the env scales
+ * by 10 and does not clip, vectorized_env.py:69-70), obs [A][D] post-auto-reset, rew [A],
+ * done [A].  rew/done/obs may be NULL to skip writing them. */
+int fenv_step(fenv_t *env, const float *act, float *obs, float *rew, uint8_t *done,
+              void *stream);
+
+/* T consecutive env.step calls fused in one launch (state kept on chip): act [T][A][2],
+ * obs [T][A][D] (obs[k] = observation returned by step k), rew [T][A], done [T][A].
+ * Bit-identical to T fenv_step calls.  partial (may be NULL) receives per-wavefront
+ * {sum reward, sum done} pairs for fenv_reduce_partials. */
+int fenv_rollout(fenv_t *env, int32_t T, const float *act, float *obs, float *rew,
+                 uint8_t *done, float *partial, void *stream);
+
+/* Number of float2 partial records fenv_rollout writes (one per wavefront/workgroup). */
+int64_t fenv_partial_count(const fenv_t *env);
+
+/* Deterministic fixed-order reduction of `count` partial records into out[2] (double, device):
+ * {sum of rewards, sum of agent-dones}. */
+int fenv_reduce_partials(const float *partial, int64_t count, double *out, void *stream);
+
+/* compute_metrics (simulate.py:238-254) per formation on the current state, plus the
+ * per-formation mean reward logged at vectorized_env.py:80-81 (rew [A] may be NULL -> 0):
+ * out [F][4] f32 = {avg_dist_to_goal, ave_dist_to_neighbor, std_dist_to_neighbor (unbiased,
+ * NaN when N == 1), mean reward}.  sums (may be NULL) [4] double = sums of those over F. */
+int fenv_metrics(fenv_t *env, const float *rew, float *out, double *sums, void *stream);
+
+/* State access (device buffers): px,py [A], gx,gy [F], t [F] = steps_since_reset.
+ * fenv_set_state synchronises `stream` to read back t; in FENV_RESET_MT19937 mode all t
+ * must be equal (the reference keeps formations in lock-step) or FENV_EINVAL is returned. */
+int fenv_get_state(fenv_t *env, float *px, float *py, float *gx, float *gy, int32_t *t,
+                   void *stream);
+int fenv_set_state(fenv_t *env, const float *px, const float *py, const float *gx,
+                   const float *gy, const int32_t *t, void *stream);
+
+/* Host-only (no GPU needed): the reset positions the reference's global MT19937 stream gives
+ * formations [first, first+count) of a draw set of `total` formations that starts `skip_sets`
+ * draw sets after torch.manual_seed(seed).  px,py [count*N], gx,gy [count] host buffers. */
+int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64_t first,
+                          int64_t count, int32_t num_agents, float *px_host, float *py_host,
+                          float *gx_host, float *gy_host);
+
+/* Host-only: the fp32 desired neighbour distance the reference uses (simulate.py:26). */
+float fenv_desired_neighbor_dist(int32_t num_agents);
+
+/* ------------------------------------------------------------------ policy (SB3 MlpPolicy)
+ * Actor-critic MLP forward as SB3's ActorCriticPolicy with default net_arch for a Box action
+ * space: pi: D->64->64 (tanh) -> mu[2]; vf: D->64->64 (tanh) -> value; action =
+ * mu + exp(log_std) * eps, log_prob = sum_j Normal(mu_j, exp(log_std_j)).log_prob(action_j),
+ * clipped = clamp(action, -1, 1) (what collect_rollouts hands to env.step).
+ *
+ * params: flat f32 buffer (device) in the order of policy_param_layout():
+ *   pi0.W[64][D] pi0.b[64] pi2.W[64][64] pi2.b[64] vf0.W[64][D] vf0.b[64] vf2.W[64][64]
+ *   vf2.b[64] act.W[2][64] act.b[2] val.W[1][64] val.b[1] log_std[2]
+ * obs [B][D]; outputs (each may be NULL): mu [B][2], value [B], action [B][2] (unclipped
+ * sample, or mu if deterministic), logp [B], clipped [B][2].  eps ~ N(0,1) from Philox keyed
+ * by (seed, counter offset `offset`, row). */
+int policy_param_count(int32_t obs_dim);
+int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B,
+                   float *mu, float *value, float *action, float *logp, float *clipped,
+                   uint64_t seed, uint64_t offset, int32_t deterministic, void *stream);
+
+const char *fenv_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FENV_H */

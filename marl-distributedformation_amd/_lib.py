@@ -1,0 +1,115 @@
+"""ctypes binding of libfenv.so (C ABI declared in include/fenv.h).
+
+The library is the only compute path: there is no CPU fallback.  If ``libfenv.so`` is missing,
+or no HIP device is visible, every entry point raises.  torch is imported first so that the
+library binds to the HIP runtime torch has already loaded (one runtime per process).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must precede loading libfenv.so: shared HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfenv.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "fenv.h")
+
+FENV_RESET_MT19937 = 0
+FENV_RESET_PHILOX = 1
+RESET_MODES = {"mt19937": FENV_RESET_MT19937, "philox": FENV_RESET_PHILOX}
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "fenv_create": (_I32, [ctypes.POINTER(_P), _I32, _I64, _I32, _I32, ctypes.c_double, _I32,
+                           _U32, _I32, _I64, _I64]),
+    "fenv_destroy": (_I32, [_P]),
+    "fenv_info": (_I32, [_P, _P]),
+    "fenv_reset": (_I32, [_P, _P, _P]),
+    "fenv_observe": (_I32, [_P, _P, _P]),
+    "fenv_step": (_I32, [_P, _P, _P, _P, _P, _P]),
+    "fenv_rollout": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
+    "fenv_partial_count": (_I64, [_P]),
+    "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
+    "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),
+    "fenv_get_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
+    "fenv_set_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
+    "fenv_host_reset_draws": (_I32, [_U32, _I64, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
+    "fenv_desired_neighbor_dist": (ctypes.c_float, [_I32]),
+    "fenv_fp_probe": (_I32, [_I32, _P, _P, _P, _I64, _P]),
+    "policy_param_count": (_I32, [_I32]),
+    "policy_forward": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _U64, _U64, _I32, _P]),
+    "fenv_last_error": (ctypes.c_char_p, []),
+}
+
+
+class FenvError(RuntimeError):
+    """A libfenv.so call returned an error code."""
+
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER) -> list[str]:
+    """Function names declared in include/fenv.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*([a-z_0-9]+)\s*\(", src,
+                                 flags=re.M)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libfenv.so (raises ImportError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: the formation env has no CPU fallback. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C marl-distributedformation_amd/csrc`.")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().fenv_last_error().decode(errors="replace")
+        raise FenvError(f"{what or 'libfenv'} failed (code {rc}): {msg}")
+
+
+def ptr(t) -> ctypes.c_void_p | None:
+    """Raw data pointer of a torch tensor / numpy array (None passes NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return ctypes.c_void_p(t.data_ptr())
+    return t.ctypes.data_as(ctypes.c_void_p)
+
+
+def current_stream(device: torch.device | int | None = None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(device=None) -> torch.device:
+    """The HIP device the env runs on; raise loudly when there is none (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible: the MI355X formation env has no CPU path "
+                           "(the CPU restatement under oracle/ is a test checker, not a fallback)")
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+    if d.type != "cuda":
+        raise ValueError(f"FormationEnv device must be a HIP device, got {d}")
+    return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())

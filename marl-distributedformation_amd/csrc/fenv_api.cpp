@@ -1,0 +1,373 @@
+// C-ABI host layer of libfenv.so (include/fenv.h): handle lifecycle, the reference's global
+// MT19937 reset stream (torch.manual_seed + torch.rand, simulate.py:125,133,140) replayed on the
+// host and staged to HBM, launch splitting at reset events, and error reporting.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "fenv.h"
+#include "fenv_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define FENV_HIP(expr)                                                                  \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(FENV_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// torch.rand float32 from one 32-bit MT19937 draw.
+inline float u24(uint32_t r) { return (float)(r & 0xFFFFFFu) * 0x1.0p-24f; }
+
+// One formation's reset draws (simulate.py:133-143): N (x, y) pairs then the goal pair.
+inline void draw_formation(std::mt19937 &mt, int32_t N, float *px, float *py, float &gx,
+                           float &gy) {
+    for (int32_t j = 0; j < N; ++j) {
+        const float ux = u24(mt());
+        const float uy = u24(mt());
+        px[j] = ux * 400.0f;
+        py[j] = uy * 100.0f;
+    }
+    const float g0 = u24(mt());
+    const float g1 = u24(mt());
+    gx = g0 * 280.0f + 60.0f;
+    gy = g1 * 480.0f + 60.0f;
+}
+
+}  // namespace
+
+struct fenv {
+    int32_t device = 0;
+    fenvk::Consts c{};
+    int32_t D = 8;
+    int32_t goal_in_obs = 1;
+    uint32_t seed = 0;
+    int64_t total = 0;  // formations in the whole (unsharded) batch
+    int64_t A = 0;
+    fenvk::DevState s{};
+    float *pend = nullptr;   // device: px[A] py[A] gx[F] gy[F] of the next MT reset event
+    float *hpend = nullptr;  // pinned host staging for `pend`
+    hipEvent_t pend_ev = nullptr;
+    bool pend_ev_recorded = false;
+    std::mt19937 mt;         // the reference's global stream (all formations of all shards)
+    int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
+
+    size_t pend_floats() const { return (size_t)(2 * A + 2 * c.F); }
+    fenvk::DevPending pending() const {
+        return fenvk::DevPending{pend, pend + A, pend + 2 * A, pend + 2 * A + c.F};
+    }
+
+    // Draw the next reset set of the global stream; keep this shard's part; stage it to HBM.
+    int gen_pending(hipStream_t st) {
+        if (c.reset_mode != FENV_RESET_MT19937) return FENV_OK;
+        if (pend_ev_recorded) FENV_HIP(hipEventSynchronize(pend_ev));  // staging buffer free
+        const uint64_t per = 2ull * (uint64_t)c.N + 2ull;
+        mt.discard(per * (uint64_t)c.f0);
+        float *px = hpend, *py = hpend + A, *gx = hpend + 2 * A, *gy = hpend + 2 * A + c.F;
+        for (int64_t f = 0; f < c.F; ++f)
+            draw_formation(mt, c.N, px + f * c.N, py + f * c.N, gx[f], gy[f]);
+        mt.discard(per * (uint64_t)(total - c.f0 - c.F));
+        FENV_HIP(hipMemcpyAsync(pend, hpend, pend_floats() * sizeof(float), hipMemcpyHostToDevice,
+                                st));
+        FENV_HIP(hipEventRecord(pend_ev, st));
+        pend_ev_recorded = true;
+        return FENV_OK;
+    }
+
+    // Apply a reset to every formation (pending set or Philox) and optionally write obs.
+    int apply_reset(float *obs, hipStream_t st) {
+        FENV_HIP(fenvk::launch_reset_observe(c, s, pending(), D, true, obs, st));
+        t_common = 0;
+        return gen_pending(st);
+    }
+
+    void advance_t(int64_t T) {
+        if (t_common < 0) return;
+        for (int64_t k = 0; k < T; ++k) t_common = (t_common > c.max_steps) ? 0 : t_common + 1;
+    }
+};
+
+extern "C" {
+
+const char *fenv_last_error(void) { return g_err.c_str(); }
+
+float fenv_desired_neighbor_dist(int32_t num_agents) {
+    // simulate.py:26 in float64 (numpy), rounded to fp32 where it meets the fp32 tensor.
+    return (float)(2.0 * 60.0 * std::sin(M_PI / (double)num_agents));
+}
+
+int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num_agents,
+                int32_t goal_in_obs, double share_reward_ratio, int32_t max_steps, uint32_t seed,
+                int32_t reset_mode, int64_t first_formation, int64_t total_formations) {
+    if (!out) return fail(FENV_EINVAL, "fenv_create: out is NULL");
+    *out = nullptr;
+    if (num_formation < 1) return fail(FENV_EINVAL, "num_formation must be >= 1");
+    if (num_agents < 1 || num_agents > 1024)
+        return fail(FENV_EINVAL, "num_agents_per_formation must be in [1, 1024]");
+    if (!(share_reward_ratio >= 0.0 && share_reward_ratio <= 0.5))
+        return fail(FENV_EINVAL, "share_reward_ratio must be in [0, 0.5] (simulate.py:28)");
+    if (max_steps < 0) return fail(FENV_EINVAL, "max_steps must be >= 0");
+    if (reset_mode != FENV_RESET_MT19937 && reset_mode != FENV_RESET_PHILOX)
+        return fail(FENV_EINVAL, "reset_mode must be FENV_RESET_MT19937 or FENV_RESET_PHILOX");
+    if (total_formations == 0) total_formations = num_formation;
+    if (first_formation < 0 || first_formation + num_formation > total_formations)
+        return fail(FENV_EINVAL, "shard [first, first+num_formation) outside total_formations");
+    if (num_formation * (int64_t)num_agents > (int64_t)1 << 40)
+        return fail(FENV_EINVAL, "too many agents");
+
+    int ndev = 0;
+    FENV_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(FENV_EINVAL, "device index out of range");
+    FENV_HIP(hipSetDevice(device));
+
+    fenv *e = new fenv();
+    e->device = device;
+    e->goal_in_obs = goal_in_obs ? 1 : 0;
+    e->D = goal_in_obs ? 8 : 6;  // vectorized_env.py:28-31
+    e->seed = seed;
+    e->total = total_formations;
+    e->A = num_formation * num_agents;
+    fenvk::Consts &c = e->c;
+    c.F = num_formation;
+    c.f0 = first_formation;
+    c.N = num_agents;
+    c.fpw = num_agents <= 64 ? 64 / num_agents : 1;
+    c.max_steps = max_steps;
+    c.reset_mode = reset_mode;
+    c.c_self = (float)(1.0 - 2.0 * share_reward_ratio);
+    c.c_nb = (float)share_reward_ratio;
+    c.d_nb = fenv_desired_neighbor_dist(num_agents);
+    c.key0 = seed;
+    c.key1 = 0x5EEDF00Du;
+    e->mt.seed(seed);  // == torch.manual_seed(seed) -> init_genrand(seed)
+
+    auto cleanup = [&](int code) {
+        fenv_destroy(e);
+        return code;
+    };
+    const size_t A = (size_t)e->A, F = (size_t)c.F;
+    hipError_t he = hipSuccess;
+    char *state = nullptr;
+    const size_t bytes = A * 8 + F * 16;
+    he = hipMalloc(&state, bytes);
+    if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(state) failed"));
+    e->s.px = reinterpret_cast<float *>(state);
+    e->s.py = e->s.px + A;
+    e->s.gx = e->s.py + A;
+    e->s.gy = e->s.gx + F;
+    e->s.t = reinterpret_cast<int32_t *>(e->s.gy + F);
+    e->s.ep = reinterpret_cast<uint32_t *>(e->s.t + F);
+    he = hipMemset(state, 0, bytes);
+    if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipMemset(state) failed"));
+    if (reset_mode == FENV_RESET_MT19937) {
+        he = hipMalloc(&e->pend, e->pend_floats() * sizeof(float));
+        if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
+        he = hipHostMalloc(&e->hpend, e->pend_floats() * sizeof(float), hipHostMallocDefault);
+        if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipHostMalloc(pending) failed"));
+        he = hipEventCreateWithFlags(&e->pend_ev, hipEventDisableTiming);
+        if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipEventCreate failed"));
+    }
+    // FormationEnv ctor: every FormationSimulator.__init__ calls reset() (simulate.py:61).
+    int rc = e->gen_pending(nullptr);
+    if (rc) return cleanup(rc);
+    rc = e->apply_reset(nullptr, nullptr);
+    if (rc) return cleanup(rc);
+    he = hipStreamSynchronize(nullptr);
+    if (he != hipSuccess) return cleanup(fail(FENV_EHIP, hipGetErrorString(he)));
+    *out = e;
+    return FENV_OK;
+}
+
+int fenv_destroy(fenv_t *e) {
+    if (!e) return FENV_OK;
+    (void)hipSetDevice(e->device);
+    if (e->pend_ev_recorded) (void)hipEventSynchronize(e->pend_ev);
+    if (e->s.px) (void)hipFree(e->s.px);
+    if (e->pend) (void)hipFree(e->pend);
+    if (e->hpend) (void)hipHostFree(e->hpend);
+    if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
+    delete e;
+    return FENV_OK;
+}
+
+int fenv_info(const fenv_t *e, int64_t *o) {
+    if (!e || !o) return fail(FENV_EINVAL, "fenv_info: NULL argument");
+    o[0] = e->c.F;
+    o[1] = e->c.N;
+    o[2] = e->D;
+    o[3] = e->A;
+    o[4] = e->t_common;
+    o[5] = e->c.reset_mode;
+    o[6] = e->c.f0;
+    o[7] = e->total;
+    return FENV_OK;
+}
+
+int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::group_count(e->c) : -1; }
+
+int fenv_reset(fenv_t *e, float *obs, void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_reset: NULL handle");
+    FENV_HIP(hipSetDevice(e->device));
+    return e->apply_reset(obs, as_stream(stream));
+}
+
+int fenv_observe(fenv_t *e, float *obs, void *stream) {
+    if (!e || !obs) return fail(FENV_EINVAL, "fenv_observe: NULL argument");
+    FENV_HIP(hipSetDevice(e->device));
+    FENV_HIP(fenvk::launch_reset_observe(e->c, e->s, e->pending(), e->D, false, obs,
+                                        as_stream(stream)));
+    return FENV_OK;
+}
+
+int fenv_rollout(fenv_t *e, int32_t T, const float *act, float *obs, float *rew, uint8_t *done,
+                 float *partial, void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_rollout: NULL handle");
+    if (T < 0) return fail(FENV_EINVAL, "fenv_rollout: T must be >= 0");
+    if (!act && T > 0) return fail(FENV_EINVAL, "fenv_rollout: act is NULL");
+    FENV_HIP(hipSetDevice(e->device));
+    hipStream_t st = as_stream(stream);
+    const int64_t A = e->A, D = e->D;
+    int64_t k0 = 0;
+    while (k0 < T) {
+        int64_t L = T - k0;
+        bool event = false;
+        if (e->c.reset_mode == FENV_RESET_MT19937) {
+            if (e->t_common < 0)
+                return fail(FENV_ESTATE, "MT19937 reset mode needs formations in lock-step");
+            // first local step whose pre-step t exceeds max_steps (simulate.py:231)
+            const int64_t je = std::max<int64_t>(0, (int64_t)e->c.max_steps + 1 - e->t_common);
+            if (je < L) {
+                L = je + 1;  // this launch ends with the reset event
+                event = true;
+            }
+        }
+        FENV_HIP(fenvk::launch_rollout(
+            e->c, e->s, e->pending(), (int32_t)L, (int32_t)D, act + k0 * A * 2,
+            obs ? obs + k0 * A * D : nullptr, rew ? rew + k0 * A : nullptr,
+            done ? done + k0 * A : nullptr, partial, k0 > 0, st));
+        e->advance_t(L);
+        if (event) {
+            int rc = e->gen_pending(st);
+            if (rc) return rc;
+        }
+        k0 += L;
+    }
+    return FENV_OK;
+}
+
+int fenv_step(fenv_t *e, const float *act, float *obs, float *rew, uint8_t *done, void *stream) {
+    return fenv_rollout(e, 1, act, obs, rew, done, nullptr, stream);
+}
+
+int fenv_reduce_partials(const float *partial, int64_t count, double *out, void *stream) {
+    if (!partial || !out || count < 0) return fail(FENV_EINVAL, "fenv_reduce_partials: bad args");
+    FENV_HIP(fenvk::launch_reduce_partials(partial, count, out, as_stream(stream)));
+    return FENV_OK;
+}
+
+int fenv_metrics(fenv_t *e, const float *rew, float *out, double *sums, void *stream) {
+    if (!e || !out) return fail(FENV_EINVAL, "fenv_metrics: NULL argument");
+    FENV_HIP(hipSetDevice(e->device));
+    FENV_HIP(fenvk::launch_metrics(e->c, e->s, rew, out, sums, nullptr, as_stream(stream)));
+    return FENV_OK;
+}
+
+int fenv_get_state(fenv_t *e, float *px, float *py, float *gx, float *gy, int32_t *t,
+                   void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_get_state: NULL handle");
+    FENV_HIP(hipSetDevice(e->device));
+    hipStream_t st = as_stream(stream);
+    const size_t A = (size_t)e->A, F = (size_t)e->c.F;
+    if (px) FENV_HIP(hipMemcpyAsync(px, e->s.px, A * 4, hipMemcpyDeviceToDevice, st));
+    if (py) FENV_HIP(hipMemcpyAsync(py, e->s.py, A * 4, hipMemcpyDeviceToDevice, st));
+    if (gx) FENV_HIP(hipMemcpyAsync(gx, e->s.gx, F * 4, hipMemcpyDeviceToDevice, st));
+    if (gy) FENV_HIP(hipMemcpyAsync(gy, e->s.gy, F * 4, hipMemcpyDeviceToDevice, st));
+    if (t) FENV_HIP(hipMemcpyAsync(t, e->s.t, F * 4, hipMemcpyDeviceToDevice, st));
+    return FENV_OK;
+}
+
+int fenv_set_state(fenv_t *e, const float *px, const float *py, const float *gx, const float *gy,
+                   const int32_t *t, void *stream) {
+    if (!e || !px || !py || !gx || !gy || !t) return fail(FENV_EINVAL, "fenv_set_state: NULL");
+    FENV_HIP(hipSetDevice(e->device));
+    hipStream_t st = as_stream(stream);
+    const size_t A = (size_t)e->A, F = (size_t)e->c.F;
+    std::vector<int32_t> ht(F);
+    FENV_HIP(hipMemcpyAsync(ht.data(), t, F * 4, hipMemcpyDeviceToHost, st));
+    FENV_HIP(hipStreamSynchronize(st));
+    int64_t tc = ht[0];
+    for (size_t f = 0; f < F; ++f) {
+        if (ht[f] < 0) return fail(FENV_EINVAL, "fenv_set_state: negative steps_since_reset");
+        if (ht[f] != ht[0]) tc = -1;
+    }
+    if (tc < 0 && e->c.reset_mode == FENV_RESET_MT19937)
+        return fail(FENV_EINVAL,
+                    "fenv_set_state: MT19937 reset mode replays the reference's global stream and "
+                    "needs every formation at the same steps_since_reset; use FENV_RESET_PHILOX");
+    FENV_HIP(hipMemcpyAsync(e->s.px, px, A * 4, hipMemcpyDeviceToDevice, st));
+    FENV_HIP(hipMemcpyAsync(e->s.py, py, A * 4, hipMemcpyDeviceToDevice, st));
+    FENV_HIP(hipMemcpyAsync(e->s.gx, gx, F * 4, hipMemcpyDeviceToDevice, st));
+    FENV_HIP(hipMemcpyAsync(e->s.gy, gy, F * 4, hipMemcpyDeviceToDevice, st));
+    FENV_HIP(hipMemcpyAsync(e->s.t, t, F * 4, hipMemcpyDeviceToDevice, st));
+    e->t_common = tc;
+    return FENV_OK;
+}
+
+int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64_t first,
+                          int64_t count, int32_t num_agents, float *px, float *py, float *gx,
+                          float *gy) {
+    if (num_agents < 1 || total < 0 || first < 0 || count < 0 || first + count > total ||
+        skip_sets < 0 || (count > 0 && (!px || !py || !gx || !gy)))
+        return fail(FENV_EINVAL, "fenv_host_reset_draws: bad arguments");
+    std::mt19937 mt(seed);
+    const uint64_t per = 2ull * (uint64_t)num_agents + 2ull;
+    mt.discard(per * ((uint64_t)skip_sets * (uint64_t)total + (uint64_t)first));
+    for (int64_t f = 0; f < count; ++f)
+        draw_formation(mt, num_agents, px + f * num_agents, py + f * num_agents, gx[f], gy[f]);
+    return FENV_OK;
+}
+
+// Diagnostic: run one of the kernels' fp32 primitives over n inputs on the device
+// (op 0: x/400, 1: x/600, 2: sqrtf(x), 3: sqrtf(fmaf(y, y, x*x))).  Device pointers.
+int fenv_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,
+                  void *stream) {
+    if (!a || !out || n < 0 || op < 0 || op > 3 || (op == 3 && !b))
+        return fail(FENV_EINVAL, "fenv_fp_probe: bad arguments");
+    FENV_HIP(fenvk::launch_fp_probe(op, a, b, out, n, as_stream(stream)));
+    return FENV_OK;
+}
+
+int policy_param_count(int32_t obs_dim) {
+    // 2 x (D*64 + 64 + 64*64 + 64) + (2*64 + 2) + (64 + 1) + 2 (log_std)
+    return 2 * (obs_dim * 64 + 64 + 64 * 64 + 64) + 130 + 65 + 2;
+}
+
+int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B, float *mu,
+                   float *value, float *action, float *logp, float *clipped, uint64_t seed,
+                   uint64_t offset, int32_t deterministic, void *stream) {
+    if (!params || !obs || B < 0 || (obs_dim != 6 && obs_dim != 8))
+        return fail(FENV_EINVAL, "policy_forward: bad arguments (obs_dim must be 6 or 8)");
+    if (B == 0) return FENV_OK;
+    FENV_HIP(fenvk::launch_policy_forward(params, obs_dim, obs, B, mu, value, action, logp, clipped,
+                                         seed, offset, deterministic, as_stream(stream)));
+    return FENV_OK;
+}
+
+}  // extern "C"

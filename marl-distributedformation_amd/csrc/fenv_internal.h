@@ -1,0 +1,58 @@
+// Internal interface between the C-ABI host layer (fenv_api.cpp) and the gfx950 kernels
+// (fenv_kernels.hip, policy_kernels.hip).  Not installed; the public ABI is include/fenv.h.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace fenvk {
+
+// Device-resident env state, structure-of-arrays (one lane reads 8 B of position per agent,
+// formation scalars are broadcast from one cache line to the formation's lanes).
+struct DevState {
+    float *px, *py;  // [A]  agent positions (simulate.py:133-135 self.agents)
+    float *gx, *gy;  // [F]  goal (simulate.py:140-143)
+    int32_t *t;      // [F]  steps_since_reset (simulate.py:147, :111)
+    uint32_t *ep;    // [F]  episode counter (Philox reset key; not in the reference)
+};
+
+// Host-staged next reset draw set (FENV_RESET_MT19937 mode), same layout as DevState.
+struct DevPending {
+    const float *px, *py, *gx, *gy;
+};
+
+struct Consts {
+    int64_t F;          // formations in this shard
+    int64_t f0;         // global index of formation 0 of the shard (Philox key)
+    int32_t N;          // agents per formation
+    int32_t fpw;        // formations per 64-lane wavefront (N <= 64 path)
+    int32_t max_steps;  // simulate.py:20
+    int32_t reset_mode; // FENV_RESET_*
+    float c_self, c_nb; // (1 - 2 share), share (simulate.py:228-229)
+    float d_nb;         // desired neighbour distance, fp32 (simulate.py:26)
+    uint32_t key0, key1;// Philox key
+};
+
+// Geometry: N <= 64 -> `fpw` whole formations per wavefront, 256-thread workgroups.
+//           N  > 64 -> one formation per workgroup of round_up(N, 64) threads (LDS exchange).
+inline bool wave_path(int32_t N) { return N <= 64; }
+int64_t group_count(const Consts &c);  // wavefronts (N<=64) or workgroups (N>64)
+
+hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
+                          int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
+                          float *partial, bool accumulate, hipStream_t st);
+hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPending &p,
+                                int32_t D, bool do_reset, float *obs, hipStream_t st);
+hipError_t launch_metrics(const Consts &c, const DevState &s, const float *rew, float *out,
+                          double *sums, double *scratch, hipStream_t st);
+hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
+                                  hipStream_t st);
+hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,
+                           hipStream_t st);
+
+hipError_t launch_policy_forward(const float *params, int32_t D, const float *obs, int64_t B,
+                                 float *mu, float *value, float *action, float *logp,
+                                 float *clipped, uint64_t seed, uint64_t offset,
+                                 int32_t deterministic, hipStream_t st);
+
+}  // namespace fenvk

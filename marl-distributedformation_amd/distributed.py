@@ -1,0 +1,88 @@
+"""Formation sharding across ranks (one process per GPU) and the only collectives the env path
+needs: an all-reduce of episode statistics (and, once PPO runs on device, of the flat policy
+gradient).  The reference is single-process (no torch.distributed anywhere); this is
+new, per SURVEY §8(e): formations are independent, so env stepping needs no communication.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous formation shard [first, first+count) of rank `rank` (sizes differ by <= 1)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    base, rem = divmod(int(total), int(world))
+    first = rank * base + min(rank, rem)
+    count = base + (1 if rank < rem else 0)
+    return first, count
+
+
+def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun's env vars when WORLD_SIZE > 1.
+
+    Returns (rank, world_size, local_rank).  backend defaults to "nccl" (RCCL on ROCm) when a
+    GPU is visible, else "gloo"."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+class StatsReducer:
+    """Double-buffered, stream-overlapped all-reduce of a small stats vector.
+
+    ``submit(v)`` copies v into the next slot and starts an async all-reduce on a side stream
+    (after the producing stream's work); the main stream never waits on the collective except
+    when a slot is reused two submissions later.  ``result()`` waits and returns the last sum.
+    With world_size 1 it degenerates to a copy."""
+
+    def __init__(self, n: int, device, dtype=torch.float64):
+        self.device = torch.device(device)
+        self.buf = [torch.zeros(n, dtype=dtype, device=self.device) for _ in range(2)]
+        self.work = [None, None]
+        self.k = 0
+        self.cuda = self.device.type == "cuda"
+        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self.dist = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def submit(self, v: torch.Tensor) -> None:
+        s = self.k % 2
+        if self.work[s] is not None:
+            self.work[s].wait()
+            self.work[s] = None
+        self.buf[s].copy_(v)
+        if self.dist:
+            if self.cuda:
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    self.work[s] = dist.all_reduce(self.buf[s], async_op=True)
+            else:
+                self.work[s] = dist.all_reduce(self.buf[s], async_op=True)
+        self.k += 1
+
+    def result(self) -> torch.Tensor:
+        s = (self.k - 1) % 2
+        if self.work[s] is not None:
+            self.work[s].wait()
+            self.work[s] = None
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+        return self.buf[s]
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,359 @@
+"""FormationEnv: drop-in for the reference's SB3 VecEnv (vectorized_env.py:16-109) on MI355X.
+
+Same constructor, attributes, methods and error behaviour as the reference class, with all F*N
+agents stepped by the gfx950 kernels of libfenv.so in one launch per call:
+
+=========================  ===================================================================
+reference                  here
+=========================  ===================================================================
+``FormationEnv(cfg, visualize=False, log=True)``  (:22-50)   same; extra keyword-only knobs
+``num_envs``, ``observation_space``, ``action_space``, ``obs_dim``,
+``num_agents_per_formation``, ``formationsim_list``           same (views, see simulate.py)
+``reset() -> np.float32[A, D]``  (:52-55)                     same (host copy of the device obs)
+``step(actions) -> (obs, rew, done, infos)``  (:68-82)       same; arrays alias env buffers
+``close/env_is_wrapped/set_attr/env_method/seed/step_async/step_wait`` raise NotImplementedError
+``get_attr`` raises AttributeError                             same
+=========================  ===================================================================
+
+Device faces (no PCIe per step): :meth:`step_tensor`, :meth:`rollout`, :meth:`observe_tensor`,
+:meth:`metrics`, :meth:`get_state` / :meth:`set_state`.
+
+Parity: with ``reset_mode="mt19937"`` (default) and ``seed=s`` the env reproduces, bit for bit,
+the reference constructed right after ``torch.manual_seed(s)`` (tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from collections.abc import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import as_config
+from .simulate import FormationView, FormationViewList
+
+
+class Box:
+    """Minimal stand-in for ``gymnasium.spaces.Box`` (vectorized_env.py:34-35)."""
+
+    def __init__(self, low, high, shape, dtype):
+        self.low = np.full(shape, low, dtype=dtype)
+        self.high = np.full(shape, high, dtype=dtype)
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+
+    def __repr__(self):
+        return f"Box({self.low.min()}, {self.high.max()}, {self.shape}, {self.dtype})"
+
+
+def _make_box(low, high, shape, dtype):
+    try:  # the real gymnasium space when it is installed (SB3 checks isinstance)
+        from gymnasium import spaces
+        return spaces.Box(low=low, high=high, shape=shape, dtype=dtype)
+    except Exception:
+        return Box(low, high, shape, dtype)
+
+
+class _Infos(Sequence):
+    """``infos`` list of length A: one empty dict per agent, created on first access."""
+
+    def __init__(self, n: int):
+        self._n = int(n)
+        self._d: dict[int, dict] = {}
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        i = int(i)
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        d = self._d.get(i)
+        if d is None:
+            d = self._d[i] = {}
+        return d
+
+
+class FormationEnv:
+    """Batched formation env on one HIP device (one shard of a multi-GPU batch)."""
+
+    MAX_SPEED = 10  # vectorized_env.py:69
+
+    def __init__(self, cfg, visualize: bool = False, log: bool = True, *, device=None,
+                 seed: int | None = None, reset_mode: str | None = None,
+                 max_steps: int | None = None, honor_share_reward_ratio: bool = False,
+                 first_formation: int = 0, total_formations: int | None = None):
+        cfg = as_config(cfg)
+        self.cfg = cfg
+        self.device = _lib.require_device(device if device is not None else cfg.get("device"))
+        self.num_agents_per_formation = int(cfg.num_agents_per_formation)
+        self.num_formation = int(cfg.num_formation)
+        self.goal_in_obs = bool(cfg.goal_in_obs)
+        self.obs_dim = 8 if self.goal_in_obs else 6          # vectorized_env.py:28-31
+        self.num_envs = self.num_agents_per_formation * self.num_formation  # :32
+        self.action_space = _make_box(-1, 1, (2,), np.float32)               # :34
+        self.observation_space = _make_box(-1, 1, (self.obs_dim,), np.float32)
+        # Q1: the reference never forwards cfg.share_reward_ratio (vectorized_env.py:43)
+        self.share_reward_ratio = (float(cfg.share_reward_ratio) if honor_share_reward_ratio
+                                   else 0.25)
+        self.max_steps = int(max_steps if max_steps is not None else cfg.get("max_steps", 1000))
+        if seed is None:
+            seed = cfg.get("seed", None)
+        if seed is None:  # the torch global stream the reference draws from (simulate.py:133)
+            seed = torch.initial_seed()
+        self.seed = int(seed) & 0xFFFFFFFF
+        mode = reset_mode or cfg.get("reset_mode", "mt19937")
+        if mode not in _lib.RESET_MODES:
+            raise ValueError(f"reset_mode must be one of {sorted(_lib.RESET_MODES)}")
+        self.reset_mode = mode
+        self.first_formation = int(first_formation)
+        self.total_formations = int(total_formations or self.num_formation)
+        self.visualize = bool(visualize)
+        self.log = bool(log)
+        self.desired_neighbor_dist = float(
+            _lib.lib().fenv_desired_neighbor_dist(self.num_agents_per_formation))
+
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.fenv_create(ctypes.byref(h), self.device.index, self.num_formation,
+                                     self.num_agents_per_formation, int(self.goal_in_obs),
+                                     self.share_reward_ratio, self.max_steps, self.seed,
+                                     _lib.RESET_MODES[mode], self.first_formation,
+                                     self.total_formations), "fenv_create")
+        self._h = h
+        A, D, F = self.num_envs, self.obs_dim, self.num_formation
+        dev = self.device
+        # device buffers (vectorized_env.py:46-48 obs_buf / reward_buf / done_buf)
+        self.obs_dev = torch.zeros((A, D), dtype=torch.float32, device=dev)
+        self.rew_dev = torch.zeros(A, dtype=torch.float32, device=dev)
+        self.done_dev = torch.zeros(A, dtype=torch.bool, device=dev)
+        self._act_dev = torch.zeros((A, 2), dtype=torch.float32, device=dev)
+        self._host = None  # pinned host mirrors, created on first numpy call
+        self.infos = _Infos(A)                                # vectorized_env.py:49
+        self.formationsim_list = FormationViewList(self, F)  # vectorized_env.py:38
+        self._fig = None
+        if self.visualize:
+            from .viz import FormationFigure
+            self._fig = FormationFigure(self.num_agents_per_formation)
+            self._refresh_fig()
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return _lib.current_stream(self.device)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().fenv_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def _ensure_host(self):
+        if self._host is None:
+            A, D = self.num_envs, self.obs_dim
+            pin = torch.cuda.is_available()
+            self._host = dict(
+                obs=torch.zeros((A, D), dtype=torch.float32, pin_memory=pin),
+                rew=torch.zeros(A, dtype=torch.float32, pin_memory=pin),
+                done=torch.zeros(A, dtype=torch.bool, pin_memory=pin),
+                act=torch.zeros((A, 2), dtype=torch.float32, pin_memory=pin),
+            )
+        return self._host
+
+    def _make_view(self, i: int) -> FormationView:
+        v = FormationView(self, i)
+        if i == 0 and self._fig is not None:
+            v.visualize = True
+            v.fig = self._fig.fig
+            v.ax = self._fig.ax
+        return v
+
+    def _formation_state(self, i: int):
+        N = self.num_agents_per_formation
+        px, py, gx, gy, t = self.get_state()
+        sl = slice(i * N, (i + 1) * N)
+        return (px[sl].cpu().numpy(), py[sl].cpu().numpy(), float(gx[i]), float(gy[i]),
+                int(t[i]))
+
+    def _refresh_fig(self):
+        if self._fig is None:
+            return
+        px, py, gx, gy, _ = self._formation_state(0)
+        self._fig.update(px, py, gx, gy)
+
+    def info(self) -> dict:
+        out = (ctypes.c_int64 * 8)()
+        _lib.check(_lib.lib().fenv_info(self._h, out), "fenv_info")
+        keys = ["num_formation", "num_agents", "obs_dim", "num_agents_total",
+                "steps_since_reset", "reset_mode", "first_formation", "total_formations"]
+        return dict(zip(keys, list(out)))
+
+    # ------------------------------------------------------------------ reference API
+    def reset(self) -> np.ndarray:
+        """vectorized_env.py:52-55: reset every formation and return obs [A, D] (numpy)."""
+        self.reset_tensor()
+        return self._to_host_obs()
+
+    def compute_observations(self) -> np.ndarray:
+        """vectorized_env.py:57-66 (numpy view of the current observations)."""
+        self.observe_tensor()
+        return self._to_host_obs()
+
+    def step(self, actions):
+        """vectorized_env.py:68-82.  ``actions`` [A, 2] in the action space (numpy or tensor).
+
+        Returns ``(obs, rewards, dones, infos)`` as numpy arrays that alias this env's host
+        buffers (overwritten by the next call, like the reference's ``obs_buf.numpy()``)."""
+        if isinstance(actions, torch.Tensor) and actions.is_cuda:
+            act = actions
+        else:
+            a = np.asarray(actions, dtype=np.float32)
+            if a.shape != (self.num_envs, 2):
+                # simulate.py:79 asserts input_velocity.shape == agents.shape per formation
+                raise AssertionError(f"actions shape {a.shape} != {(self.num_envs, 2)}")
+            host = self._ensure_host()
+            host["act"].numpy()[...] = a
+            self._act_dev.copy_(host["act"], non_blocking=True)
+            act = self._act_dev
+        self.step_tensor(act)
+        host = self._ensure_host()
+        host["obs"].copy_(self.obs_dev, non_blocking=True)
+        host["rew"].copy_(self.rew_dev, non_blocking=True)
+        host["done"].copy_(self.done_dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        if self._fig is not None:
+            self._refresh_fig()
+        return host["obs"].numpy(), host["rew"].numpy(), host["done"].numpy(), self.infos
+
+    def close(self):
+        raise NotImplementedError
+
+    def env_is_wrapped(self, wrapper_class):
+        raise NotImplementedError
+
+    def get_attr(self, attr_name, indices=None):
+        raise AttributeError
+
+    def set_attr(self, attr_name, value, indices=None):
+        raise NotImplementedError
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        raise NotImplementedError
+
+    def seed(self, seed=None):
+        raise NotImplementedError
+
+    def step_wait(self):
+        raise NotImplementedError
+
+    def step_async(self, actions):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ device faces
+    def _to_host_obs(self) -> np.ndarray:
+        host = self._ensure_host()
+        host["obs"].copy_(self.obs_dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        if self._fig is not None:
+            self._refresh_fig()
+        return host["obs"].numpy()
+
+    def reset_tensor(self) -> torch.Tensor:
+        """Reset every formation; returns the device obs buffer [A, D]."""
+        _lib.check(_lib.lib().fenv_reset(self._h, _lib.ptr(self.obs_dev), self._stream()),
+                   "fenv_reset")
+        return self.obs_dev
+
+    def observe_tensor(self) -> torch.Tensor:
+        _lib.check(_lib.lib().fenv_observe(self._h, _lib.ptr(self.obs_dev), self._stream()),
+                   "fenv_observe")
+        return self.obs_dev
+
+    def _check_act(self, act: torch.Tensor, lead: tuple) -> torch.Tensor:
+        shape = lead + (self.num_envs, 2)
+        if tuple(act.shape) != shape:
+            raise AssertionError(f"actions shape {tuple(act.shape)} != {shape}")
+        if act.dtype != torch.float32 or act.device != self.device:
+            raise TypeError(f"actions must be float32 on {self.device}")
+        return act.contiguous()
+
+    def step_tensor(self, actions: torch.Tensor, obs=None, rew=None, done=None):
+        """One env step on device tensors; returns (obs [A,D], rew [A], done [A] bool)."""
+        act = self._check_act(actions, ())
+        obs = self.obs_dev if obs is None else obs
+        rew = self.rew_dev if rew is None else rew
+        done = self.done_dev if done is None else done
+        _lib.check(_lib.lib().fenv_step(self._h, _lib.ptr(act), _lib.ptr(obs), _lib.ptr(rew),
+                                        _lib.ptr(done), self._stream()), "fenv_step")
+        return obs, rew, done
+
+    def rollout(self, actions: torch.Tensor, obs=None, rew=None, done=None, partial=None):
+        """T fused env steps: actions [T, A, 2] -> obs [T, A, D], rew [T, A], done [T, A].
+
+        Identical to T calls of :meth:`step_tensor`; state stays on chip for the whole launch."""
+        T = int(actions.shape[0])
+        act = self._check_act(actions, (T,))
+        A, D, dev = self.num_envs, self.obs_dim, self.device
+        if obs is None:
+            obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
+        if rew is None:
+            rew = torch.empty((T, A), dtype=torch.float32, device=dev)
+        if done is None:
+            done = torch.empty((T, A), dtype=torch.bool, device=dev)
+        _lib.check(_lib.lib().fenv_rollout(self._h, T, _lib.ptr(act), _lib.ptr(obs),
+                                           _lib.ptr(rew), _lib.ptr(done), _lib.ptr(partial),
+                                           self._stream()), "fenv_rollout")
+        return obs, rew, done
+
+    def partial_count(self) -> int:
+        return int(_lib.lib().fenv_partial_count(self._h))
+
+    def reduce_partials(self, partial: torch.Tensor, out: torch.Tensor | None = None):
+        """Sum the per-wavefront {reward, done} records of :meth:`rollout` -> double[2]."""
+        if out is None:
+            out = torch.empty(2, dtype=torch.float64, device=self.device)
+        _lib.check(_lib.lib().fenv_reduce_partials(_lib.ptr(partial), self.partial_count(),
+                                                   _lib.ptr(out), self._stream()),
+                   "fenv_reduce_partials")
+        return out
+
+    def metrics(self, rew: torch.Tensor | None = None, sums: torch.Tensor | None = None):
+        """simulate.py:238-254 per formation (+ mean reward): device tensor [F, 4]."""
+        out = torch.empty((self.num_formation, 4), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().fenv_metrics(self._h, _lib.ptr(rew), _lib.ptr(out), _lib.ptr(sums),
+                                           self._stream()), "fenv_metrics")
+        return out
+
+    def get_state(self):
+        """(px [A], py [A], gx [F], gy [F], steps_since_reset [F]) as device tensors."""
+        A, F, dev = self.num_envs, self.num_formation, self.device
+        px = torch.empty(A, dtype=torch.float32, device=dev)
+        py = torch.empty(A, dtype=torch.float32, device=dev)
+        gx = torch.empty(F, dtype=torch.float32, device=dev)
+        gy = torch.empty(F, dtype=torch.float32, device=dev)
+        t = torch.empty(F, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().fenv_get_state(self._h, *(_lib.ptr(v) for v in (px, py, gx, gy, t)),
+                                             self._stream()), "fenv_get_state")
+        return px, py, gx, gy, t
+
+    def set_state(self, px, py, gx, gy, t) -> None:
+        dev = self.device
+        vals = [torch.as_tensor(v, dtype=torch.float32).to(dev).contiguous()
+                for v in (px, py, gx, gy)]
+        tt = torch.as_tensor(t, dtype=torch.int32).to(dev).contiguous()
+        A, F = self.num_envs, self.num_formation
+        for v, n in zip(vals, (A, A, F, F)):
+            if v.numel() != n:
+                raise ValueError("set_state: wrong sizes")
+        if tt.numel() != F:
+            raise ValueError("set_state: wrong sizes")
+        _lib.check(_lib.lib().fenv_set_state(self._h, *(_lib.ptr(v) for v in vals), _lib.ptr(tt),
+                                             self._stream()), "fenv_set_state")

@@ -1,0 +1,110 @@
+"""The C-ABI library (CPU-only checks: no kernel launches).
+
+* libfenv.so loads and exports every function include/fenv.h declares;
+* its host-side pieces (the reference's global MT19937 reset stream, desired neighbour
+  distance) agree with the oracle;
+* with no HIP device every env entry point fails loudly (no CPU fallback exists).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import COracleEnv, desired_neighbor_dist, mt_raw, torch_rand_from_raw
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_symbols_exported(flib):
+    L = flib.lib()
+    names = flib.header_symbols()
+    assert "fenv_create" in names and "policy_forward" in names and "fenv_rollout" in names
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/fenv.h but not exported"
+    out = subprocess.run(["nm", "-D", "--defined-only", flib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    # the library carries gfx950 code objects only
+    blob = open(flib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_signatures_cover_header(flib):
+    assert set(flib.header_symbols()) <= set(flib.SIGNATURES)
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 7, 10, 64, 100, 1024])
+def test_desired_neighbor_dist(flib, N):
+    assert np.float32(flib.lib().fenv_desired_neighbor_dist(N)) == desired_neighbor_dist(N)
+
+
+@pytest.mark.parametrize("N,total,first,count,skip", [(5, 7, 0, 7, 0), (5, 7, 2, 3, 1),
+                                                      (10, 4, 3, 1, 2), (64, 3, 1, 2, 0),
+                                                      (1, 9, 4, 5, 3)])
+def test_host_reset_draws_match_torch_stream(flib, N, total, first, count, skip):
+    """Draw set `skip` of the global stream, restricted to formations [first, first+count),
+    equals torch.rand after torch.manual_seed (the reference's RNG, simulate.py:133-143)."""
+    seed = 4242
+    px = np.zeros(count * N, np.float32)
+    py = np.zeros(count * N, np.float32)
+    gx = np.zeros(count, np.float32)
+    gy = np.zeros(count, np.float32)
+    flib.check(flib.lib().fenv_host_reset_draws(seed, skip, total, first, count, N,
+                                                *(flib.ptr(v) for v in (px, py, gx, gy))))
+    per = 2 * N + 2
+    g = torch.Generator().manual_seed(seed)
+    allu = torch.rand(per * total * (skip + 1), generator=g).numpy()
+    u = allu[per * total * skip:].reshape(total, per)[first:first + count]
+    np.testing.assert_array_equal(px, (u[:, 0:2 * N:2] * np.float32(400)).reshape(-1))
+    np.testing.assert_array_equal(py, (u[:, 1:2 * N:2] * np.float32(100)).reshape(-1))
+    np.testing.assert_array_equal(gx, u[:, -2] * np.float32(280) + np.float32(60))
+    np.testing.assert_array_equal(gy, u[:, -1] * np.float32(480) + np.float32(60))
+    raw = mt_raw(seed, per * total * (skip + 1))
+    assert np.array_equal(torch_rand_from_raw(raw), allu)
+
+
+def test_host_reset_draws_equal_oracle_ctor_state(flib):
+    F, N, seed = 6, 5, 77
+    px = np.zeros(F * N, np.float32)
+    py = np.zeros(F * N, np.float32)
+    gx = np.zeros(F, np.float32)
+    gy = np.zeros(F, np.float32)
+    flib.check(flib.lib().fenv_host_reset_draws(seed, 0, F, 0, F, N,
+                                                *(flib.ptr(v) for v in (px, py, gx, gy))))
+    o = COracleEnv(F, N, True, seed).get_state()
+    for a, b in zip((px, py, gx, gy), o[:4]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_bad_arguments_rejected_without_device(flib):
+    L = flib.lib()
+    assert L.fenv_host_reset_draws(1, 0, 2, 1, 5, 5, None, None, None, None) == -1
+    assert b"bad arguments" in L.fenv_last_error()
+    assert L.fenv_reduce_partials(None, 1, None, None) == -1
+    assert L.policy_forward(None, 8, None, 1, None, None, None, None, None, 0, 0, 0, None) == -1
+    assert L.policy_param_count(8) == 9669  # SURVEY §8(a) R10 (incl. log_std[2])
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device failure path")
+def test_create_fails_loudly_without_device(flib, venv):
+    L = flib.lib()
+    h = ctypes.c_void_p()
+    rc = L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.25, 1000, 0, 0, 0, 4)
+    assert rc != 0 and not h.value
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        venv.FormationEnv({"num_formation": 2, "num_agents_per_formation": 5,
+                           "goal_in_obs": True})
+
+
+def test_invalid_config_rejected(flib):
+    L = flib.lib()
+    h = ctypes.c_void_p()
+    assert L.fenv_create(ctypes.byref(h), 0, 4, 0, 1, 0.25, 1000, 0, 0, 0, 4) == -1
+    assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.75, 1000, 0, 0, 0, 4) == -1
+    assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.25, 1000, 0, 7, 0, 4) == -1
+    assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.25, 1000, 0, 0, 2, 4) == -1

@@ -1,0 +1,320 @@
+"""GPU parity: the HIP env (through the C ABI) against the reference's golden fixtures and the
+CPU oracle.  fp32 results must match bit for bit (stricter than the north star's 1e-5
+relative); dones exactly."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+from oracle import COracleEnv, synth_actions
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+CASES = gu.case_names()
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+def make_env(venv, F, N, goal=True, seed=0, **kw):
+    cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": goal}
+    return venv.FormationEnv(cfg, device=DEV, seed=seed, **kw)
+
+
+class NumpyFace:
+    """Wrap FormationEnv so get_state() returns numpy (golden_util's interface)."""
+
+    def __init__(self, env):
+        self.env = env
+
+    def reset(self):
+        return self.env.reset().copy()
+
+    def step(self, a):
+        o, r, d, i = self.env.step(a)
+        return o.copy(), r.copy(), d.copy(), i
+
+    def get_state(self):
+        return tuple(v.cpu().numpy() for v in self.env.get_state())
+
+
+class RolloutFace(NumpyFace):
+    """Feeds fixture steps through fenv_rollout in chunks of `chunk` steps (buffered)."""
+
+    def __init__(self, env, case, chunk):
+        super().__init__(env)
+        self.case, self.chunk, self.buf, self.k = case, chunk, [], 0
+        self.state_after = {}
+
+    def step(self, a):
+        if not self.buf:
+            c = self.case
+            ks = range(self.k + 1, min(self.k + self.chunk, c["steps"]) + 1)
+            acts = np.stack([synth_actions(c["act_seed"], k, c["A"], c["amp"]) for k in ks])
+            obs, rew, done = self.env.rollout(torch.from_numpy(acts).to(DEV))
+            self.buf = list(zip(obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()))
+            self.state_at_chunk_end = super().get_state()
+            self.chunk_end = self.k + len(ks)
+        self.k += 1
+        o, r, d = self.buf.pop(0)
+        return o, r, d, None
+
+    def get_state(self):
+        return self.state_at_chunk_end if self.k == self.chunk_end else None
+
+
+def test_native_library_is_loaded(venv, flib):
+    env = make_env(venv, 2, 5)
+    env.reset()
+    maps = open("/proc/self/maps").read()
+    assert flib.LIB_PATH in maps, "libfenv.so not mapped: the HIP path did not run"
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_replay_step(venv, name):
+    c = gu.load_case(name)
+    gu.replay(c, lambda c: NumpyFace(make_env(venv, c["F"], c["N"], c["goal_in_obs"], c["seed"])))
+
+
+@pytest.mark.parametrize("name", ["f4_n5_d8", "f2_n64_d8", "f3_n100_d8", "f5_n1_d8",
+                                  "f1_n5_d8_walls", "f3_n10_d6"])
+@pytest.mark.parametrize("chunk", [7, 1002, 3000])
+def test_golden_replay_rollout(venv, name, chunk):
+    c = gu.load_case(name)
+    env = make_env(venv, c["F"], c["N"], c["goal_in_obs"], c["seed"])
+    face = RolloutFace(env, c, chunk)
+    # state is only observable at chunk ends; check obs/reward/done digests at every step
+    o = face.reset()
+    assert np.array_equal(bits(o), bits(c["obs_reset"]))
+    for k in range(1, c["steps"] + 1):
+        obs, rew, done, _ = face.step(None)
+        dig = c["digest"][k - 1]
+        assert gu.d64(obs) == dig[0], f"obs step {k}"
+        assert gu.d64(rew) == dig[1], f"rew step {k}"
+        assert gu.d64(done.astype(np.bool_)) == dig[2], f"done step {k}"
+        st = face.get_state()
+        if st is not None:
+            px, py, gx, gy, t = st
+            ag = np.stack([px, py], 1).reshape(-1)
+            gl = np.stack([gx, gy], 1).reshape(-1)
+            assert gu.d64(ag) == dig[3] and gu.d64(gl, t.astype(np.int32)) == dig[4], k
+
+
+def run_vs_oracle(venv, F, N, goal, seed, steps, chunks, amp=1.2, max_steps=1000, share=None,
+                  reset_mode="mt19937"):
+    kw = dict(max_steps=max_steps, reset_mode=reset_mode)
+    if share is not None:
+        env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                                 "goal_in_obs": goal, "share_reward_ratio": share},
+                                device=DEV, seed=seed, honor_share_reward_ratio=True, **kw)
+    else:
+        env = make_env(venv, F, N, goal, seed, **kw)
+    ref = COracleEnv(F, N, goal, seed, share=0.25 if share is None else share,
+                     max_steps=max_steps)
+    A = F * N
+    assert np.array_equal(bits(env.reset()), bits(ref.reset()))
+    k = 0
+    ci = 0
+    while k < steps:
+        T = min(chunks[ci % len(chunks)], steps - k)
+        ci += 1
+        acts = np.stack([synth_actions(seed + 1, k + j, A, amp) for j in range(T)])
+        obs, rew, done = env.rollout(torch.from_numpy(acts).to(DEV))
+        obs, rew, done = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        for j in range(T):
+            ro, rr, rd, _ = ref.step(acts[j])
+            assert np.array_equal(bits(obs[j]), bits(ro)), f"obs step {k + j + 1}"
+            assert np.array_equal(bits(rew[j]), bits(rr)), f"rew step {k + j + 1}"
+            assert np.array_equal(done[j], rd), f"done step {k + j + 1}"
+        k += T
+        st = [v.cpu().numpy() for v in env.get_state()]
+        for a, b in zip(st, ref.get_state()):
+            assert np.array_equal(bits(a), bits(b)), f"state after step {k}"
+    return env, ref
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 7, 10, 12, 21, 32, 33, 63, 64, 65, 100, 128, 257,
+                               1000, 1024])
+def test_all_formation_sizes_vs_oracle(venv, N):
+    F = max(3, 1200 // N)
+    run_vs_oracle(venv, F, N, True, 100 + N, steps=60, chunks=[1, 5, 23], max_steps=17)
+
+
+@pytest.mark.parametrize("goal", [True, False])
+def test_config2_size_vs_oracle(venv, goal):
+    """BASELINE config 2 (4096 formations x 5) across the 1002-step episode boundary."""
+    run_vs_oracle(venv, 4096, 5, goal, 9, steps=1010, chunks=[10, 333, 1, 700])
+
+
+@pytest.mark.parametrize("share", [0.0, 0.1, 0.4, 0.5])
+def test_share_reward_ratio_honoured(venv, share):
+    run_vs_oracle(venv, 50, 6, True, 3, steps=30, chunks=[4, 9], max_steps=12, share=share)
+
+
+def test_out_of_bounds_heavy(venv):
+    run_vs_oracle(venv, 200, 5, True, 5, steps=120, chunks=[13], amp=40.0, max_steps=50)
+
+
+def test_sharded_mt_equals_unsharded(venv):
+    F, N, total = 7, 5, 23
+    full = make_env(venv, total, N, True, 11, max_steps=9)
+    shard = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                               "goal_in_obs": True}, device=DEV, seed=11, max_steps=9,
+                              first_formation=5, total_formations=total)
+    of, osh = full.reset(), shard.reset()
+    assert np.array_equal(bits(of[5 * N:12 * N]), bits(osh))
+    for k in range(40):
+        a = synth_actions(2, k, total * N, 1.0)
+        o1, r1, d1, _ = full.step(a)
+        o2, r2, d2, _ = shard.step(a[5 * N:12 * N])
+        assert np.array_equal(bits(o1[5 * N:12 * N]), bits(o2)), k
+        assert np.array_equal(bits(r1[5 * N:12 * N]), bits(r2)), k
+        assert np.array_equal(d1[5 * N:12 * N], d2), k
+
+
+def test_philox_mode(venv):
+    F, N, total = 300, 5, 900
+    env = make_env(venv, F, N, True, 5, reset_mode="philox", max_steps=5,
+                   first_formation=300, total_formations=total)
+    full = make_env(venv, total, N, True, 5, reset_mode="philox", max_steps=5)
+    o = env.reset()
+    of = full.reset()
+    assert np.array_equal(bits(o), bits(of[300 * N:600 * N]))   # sharding invariance
+    px, py, gx, gy, t = (v.cpu().numpy() for v in env.get_state())
+    assert px.min() >= 0 and px.max() < 400 and py.min() >= 0 and py.max() < 100
+    assert gx.min() >= 60 and gx.max() < 340 and gy.min() >= 60 and gy.max() < 540
+    assert np.all(t == 0)
+    # between resets the dynamics are the reference's: compare against the oracle from the
+    # same state
+    ref = COracleEnv(F, N, True, 0, max_steps=5)
+    ref.set_state(px, py, gx, gy, t)
+    for k in range(6):
+        a = synth_actions(9, k, F * N, 1.0)
+        o1, r1, d1, _ = env.step(a)
+        o2, r2, d2, _ = ref.step(a)
+        assert np.array_equal(bits(r1), bits(r2)) and np.array_equal(d1, d2), k
+        if not d1.any():
+            assert np.array_equal(bits(o1), bits(o2)), k
+    # step 7 crosses the reset: positions redrawn in range, different from before
+    o1, r1, d1, _ = env.step(synth_actions(9, 6, F * N, 1.0))
+    assert d1.all()
+    px2, py2, _, _, t2 = (v.cpu().numpy() for v in env.get_state())
+    assert np.all(t2 == 0) and py2.max() < 100 and not np.array_equal(px2, px)
+    # deterministic in the seed
+    e2 = make_env(venv, F, N, True, 5, reset_mode="philox", first_formation=300,
+                  total_formations=total)
+    assert np.array_equal(bits(e2.reset()), bits(o))
+
+
+def test_state_roundtrip_and_lockstep_rule(venv, flib):
+    env = make_env(venv, 10, 5, True, 1)
+    env.reset()
+    px, py, gx, gy, t = env.get_state()
+    env.set_state(px + 1, py, gx, gy, t + 3)
+    p2 = env.get_state()
+    assert torch.equal(p2[0], px + 1) and torch.equal(p2[4], t + 3)
+    assert env.info()["steps_since_reset"] == 3
+    t_bad = t.clone()
+    t_bad[0] += 1
+    with pytest.raises(flib.FenvError, match="same steps_since_reset"):
+        env.set_state(px, py, gx, gy, t_bad)
+    ep = make_env(venv, 10, 5, True, 1, reset_mode="philox")
+    ep.set_state(px, py, gx, gy, t_bad)
+    assert ep.info()["steps_since_reset"] == -1
+
+
+def test_metrics_and_partials(venv):
+    F, N = 500, 5
+    env = make_env(venv, F, N, True, 21, max_steps=3)
+    ref = COracleEnv(F, N, True, 21, max_steps=3)
+    env.reset()
+    ref.reset()
+    acts = np.stack([synth_actions(4, k, F * N, 1.0) for k in range(8)])
+    partial = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
+    obs, rew, done = env.rollout(torch.from_numpy(acts).to(DEV), partial=partial)
+    rs, ds = 0.0, 0.0
+    for k in range(8):
+        _, rr, rd, _ = ref.step(acts[k])
+        rs += rr.astype(np.float64).sum()
+        ds += rd.sum()
+    sums = env.reduce_partials(partial).cpu().numpy()
+    np.testing.assert_allclose(sums[0], rs, rtol=1e-5)
+    assert sums[1] == ds
+    m = env.metrics(rew[-1]).cpu().numpy()
+    mr = ref.metrics(rew[-1].cpu().numpy())
+    np.testing.assert_allclose(m, mr, rtol=1e-5, atol=1e-4)
+    s = torch.zeros(4, dtype=torch.float64, device=DEV)
+    env.metrics(rew[-1], sums=s)
+    np.testing.assert_allclose(s.cpu().numpy(), mr.sum(0), rtol=1e-5)
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_fp_primitives_correctly_rounded(flib, op):
+    """The kernels' division / sqrt / 2-norm agree with IEEE fp32 (numpy) on 16M inputs."""
+    g = torch.Generator(device=DEV).manual_seed(op)
+    n = 1 << 24
+    a = (torch.rand(n, device=DEV, generator=g) * 1200 - 300).float()
+    a[: 1 << 20] = torch.arange(1 << 20, device=DEV, dtype=torch.float32) * (600.0 / (1 << 20))
+    b = (torch.rand(n, device=DEV, generator=g) * 1200 - 600).float()
+    if op == 2:
+        a = a.abs()
+    out = torch.empty_like(a)
+    L = flib.lib()
+    flib.check(L.fenv_fp_probe(op, flib.ptr(a), flib.ptr(b), flib.ptr(out), n, None))
+    torch.cuda.synchronize()
+    an, bn, on = a.cpu().numpy(), b.cpu().numpy(), out.cpu().numpy()
+    if op == 0:
+        ref = an / np.float32(400)
+    elif op == 1:
+        ref = an / np.float32(600)
+    elif op == 2:
+        ref = np.sqrt(an)
+    else:
+        from oracle import norm2
+        ref = norm2(an, bn)
+    assert np.array_equal(bits(on), bits(ref.astype(np.float32)))
+
+
+def test_reference_error_behaviour(venv):
+    env = make_env(venv, 3, 5)
+    with pytest.raises(AssertionError):
+        env.step(np.zeros((14, 2), np.float32))
+    with pytest.raises(AttributeError):
+        env.get_attr("x")
+    for fn in (env.close, lambda: env.seed(1), env.step_wait, lambda: env.step_async(None),
+               lambda: env.set_attr("a", 1), lambda: env.env_method("m"),
+               lambda: env.env_is_wrapped(object)):
+        with pytest.raises(NotImplementedError):
+            fn()
+    assert env.num_envs == 15 and env.obs_dim == 8
+    assert env.action_space.shape == (2,) and env.observation_space.shape == (8,)
+    _, _, _, infos = env.step(np.zeros((15, 2), np.float32))
+    assert len(infos) == 15 and infos[3] == {}
+
+
+def test_formation_views(venv):
+    env = make_env(venv, 4, 6, True, 8)
+    env.reset()
+    px, py, gx, gy, t = (v.cpu().numpy() for v in env.get_state())
+    v = env.formationsim_list[2]
+    assert len(env.formationsim_list) == 4
+    np.testing.assert_array_equal(v.agents.numpy(), np.stack([px[12:18], py[12:18]], 1))
+    np.testing.assert_array_equal(v.goal.numpy(), np.array([gx[2], gy[2]], np.float32))
+    assert v.steps_since_reset == 0 and v.num_agents == 6
+
+
+def test_visualize_mirror(venv):
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    env = venv.FormationEnv({"num_formation": 1, "num_agents_per_formation": 5,
+                             "goal_in_obs": True}, visualize=True, log=False, device=DEV, seed=3)
+    first = env.formationsim_list[0]
+    assert first.fig is not None
+    env.reset()
+    env.step(np.full((5, 2), 0.5, np.float32))
+    px, py, _, _, _ = (v.cpu().numpy() for v in env.get_state())
+    assert tuple(env._fig.dots[0].center) == (float(px[0]), float(py[0]))
