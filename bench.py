@@ -116,20 +116,34 @@ def main():
     obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
     rew = torch.empty((T, A), dtype=torch.float32, device=dev)
     done = torch.empty((T, A), dtype=torch.bool, device=dev)
-    partial = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=dev)
-    red = torch.zeros(2, dtype=torch.float64, device=dev)
+    # stats pipeline: rollout k writes partials[k%2] on the main stream; a side stream reduces
+    # them (deterministic order) and all-reduces the two doubles over RCCL, overlapped with
+    # rollout k+1; rollout k+2 waits only for the side stream to have released partials[k%2].
+    partials = [torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=dev)
+                for _ in range(2)]
+    reds = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
+    released = [None, None]
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
     stats = pdist.StatsReducer(2, dev)
     env.reset_tensor()
 
     def chunk(k, ev=None):
+        s = k % 2
+        if released[s] is not None:
+            main.wait_event(released[s])
         if ev is not None:
-            ev[0].record()
-        env.rollout(acts[k % 2], obs, rew, done, partial=None if args.no_stats else partial)
+            ev[0].record(main)
+        env.rollout(acts[k % 2], obs, rew, done, partial=None if args.no_stats else partials[s])
         if ev is not None:
-            ev[1].record()
+            ev[1].record(main)
         if not args.no_stats:
-            env.reduce_partials(partial, red)
-            stats.submit(red)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                env.reduce_partials(partials[s], reds[s])
+                stats.submit(reds[s])
+                released[s] = torch.cuda.Event()
+                released[s].record(side)
 
     warm_chunks = max(1, -(-args.warmup // T))
     n_chunks = max(1, -(-args.steps // T))
@@ -146,6 +160,7 @@ def main():
     for k in range(n_chunks):
         chunk(k, evs[k])
     if not args.no_stats:
+        main.wait_stream(side)
         tot = stats.result()
     torch.cuda.synchronize()
     if world > 1:

@@ -1,5 +1,19 @@
-// Batched actor-critic MLP forward (SB3 MlpPolicy default for a Box action space; call site
-// /root/reference/vectorized_env.py:126, /root/reference/visualize_policy.py:16).
+// Batched actor-critic MLP forward on the gfx950 matrix cores (fp32 in, fp32 accumulate).
+//
+// Reference: SB3 `PPO('MlpPolicy', env, ...)` (/root/reference/vectorized_env.py:126) builds an
+// ActorCriticPolicy with net_arch pi=[64,64], vf=[64,64], Tanh, a Linear(64,2) action head with a
+// state-independent log_std[2], and a Linear(64,1) value head; collect_rollouts samples
+// a = mu + exp(log_std) * eps, stores log_prob, and hands clip(a, -1, 1) to env.step;
+// predict(deterministic=True) (/root/reference/visualize_policy.py:16) returns clip(mu).
+//
+// Mapping (one wavefront = 32 agents per tile, persistent workgroups of 4 waves):
+//   layer 1  H1^T[64 x 32] = W1[64 x D] . O^T[D x 32]     v_mfma_f32_32x32x2_f32, 2 row tiles x D/2
+//   layer 2  H2^T[64 x 32] = W2[64 x 64] . tanh(H1^T)     the layer-1 accumulator registers ARE the
+//            B operands (lane l holds hidden rows rho(r, l>>5) of agent l&31), so no data moves
+//            between layers; W2 is read from LDS pre-permuted into that k order (ds_read_b128).
+//   heads    mu[2], value on the VALU from the layer-2 accumulators, halves joined across lanes
+//            l and l^32.
+// Both networks: 144 MFMAs of 32x32x2 per 32 agents = 18,816 FLOP/agent.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -9,10 +23,260 @@
 
 namespace fenvk {
 
-hipError_t launch_policy_forward(const float *, int32_t, const float *, int64_t, float *, float *,
-                                 float *, float *, float *, uint64_t, uint64_t, int32_t,
-                                 hipStream_t) {
-    return hipErrorNotSupported;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kHid = 64;
+
+// row of accumulator register `reg` held by lane half `h` (32x32 C/D layout)
+__host__ __device__ constexpr int rho(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// Flat parameter offsets (include/fenv.h policy_forward layout)
+struct PLayout {
+    int pi0W, pi0b, pi2W, pi2b, vf0W, vf0b, vf2W, vf2b, actW, actb, valW, valb, logstd, total;
+    __host__ __device__ explicit PLayout(int D) {
+        pi0W = 0;
+        pi0b = pi0W + kHid * D;
+        pi2W = pi0b + kHid;
+        pi2b = pi2W + kHid * kHid;
+        vf0W = pi2b + kHid;
+        vf0b = vf0W + kHid * D;
+        vf2W = vf0b + kHid;
+        vf2b = vf2W + kHid * kHid;
+        actW = vf2b + kHid;
+        actb = actW + 2 * kHid;
+        valW = actb + 2;
+        valb = valW + kHid;
+        logstd = valb + 1;
+        total = logstd + 2;
+    }
+};
+
+// LDS image (floats)
+constexpr int kW1F = 2 * 2 * 4 * 64;          // [net][ht][s][lane]
+constexpr int kW2F = 2 * 2 * 2 * 16 * 64;     // [net][ot][kt][r/4][lane][4]
+constexpr int kB = 2 * 2 * kHid;              // b1[net][64], b2[net][64]
+constexpr int kHead = 3 * kHid + 3 + 2;       // Wa[2][64], Wv[64], ba[2], bv, log_std[2]
+constexpr int kLds = kW1F + kW2F + kB + kHead;
+constexpr int oW1 = 0, oW2 = kW1F, oB1 = kW1F + kW2F, oB2 = oB1 + 2 * kHid, oHead = oB1 + kB;
+
+// Accurate single-precision tanh without libm calls: odd Taylor polynomial below 0.3,
+// 1 - 2/(1+e^{2|x|}) above (v_exp_f32 / v_rcp_f32); |rel err| < 5e-7 over all inputs.
+__device__ __forceinline__ float tanh_f(float x) {
+    const float ax = __builtin_fabsf(x);
+    const float x2 = x * x;
+    // tanh(x) = x + x^3 P(x^2), Taylor through x^13 (|x| < 0.3: truncation < 1e-10 relative)
+    float p = 21844.0f / 6081075.0f;
+    p = __builtin_fmaf(p, x2, -1382.0f / 155925.0f);
+    p = __builtin_fmaf(p, x2, 62.0f / 2835.0f);
+    p = __builtin_fmaf(p, x2, -17.0f / 315.0f);
+    p = __builtin_fmaf(p, x2, 2.0f / 15.0f);
+    p = __builtin_fmaf(p, x2, -1.0f / 3.0f);
+    const float ts = __builtin_fmaf(p, x2 * x, x);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.88539008177792681f);  // e^{2|x|}
+    const float tl = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+    return ax < 0.3f ? ts : __builtin_copysignf(tl, x);
+}
+
+__device__ __forceinline__ uint4 philox_p(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params, int32_t D,
+                                               const float *__restrict__ obs, int64_t B,
+                                               float *__restrict__ mu_out,
+                                               float *__restrict__ value_out,
+                                               float *__restrict__ act_out,
+                                               float *__restrict__ logp_out,
+                                               float *__restrict__ clip_out, uint64_t seed,
+                                               uint64_t offset, int32_t deterministic) {
+    __shared__ __attribute__((aligned(16))) float lds[kLds];
+    const PLayout L(D);
+    const int tid = threadIdx.x;
+    // ---- stage weights into the fragment-ordered LDS image
+    for (int e = tid; e < kW1F; e += blockDim.x) {
+        const int lane = e & 63, s = (e >> 6) & 3, ht = (e >> 8) & 1, net = e >> 9;
+        const int row = 32 * ht + (lane & 31), col = 2 * s + (lane >> 5);
+        const int base = net ? L.vf0W : L.pi0W;
+        lds[oW1 + e] = col < D ? params[base + row * D + col] : 0.0f;
+    }
+    for (int e = tid; e < kW2F; e += blockDim.x) {
+        const int q = e & 3, lane = (e >> 2) & 63, r4 = (e >> 8) & 3, kt = (e >> 10) & 1,
+                  ot = (e >> 11) & 1, net = e >> 12;
+        const int r = 4 * r4 + q;
+        const int row = 32 * ot + (lane & 31), col = 32 * kt + rho(r, lane >> 5);
+        lds[oW2 + e] = params[(net ? L.vf2W : L.pi2W) + row * kHid + col];
+    }
+    for (int e = tid; e < kHid; e += blockDim.x) {
+        lds[oB1 + e] = params[L.pi0b + e];
+        lds[oB1 + kHid + e] = params[L.vf0b + e];
+        lds[oB2 + e] = params[L.pi2b + e];
+        lds[oB2 + kHid + e] = params[L.vf2b + e];
+        lds[oHead + e] = params[L.actW + e];
+        lds[oHead + kHid + e] = params[L.actW + kHid + e];
+        lds[oHead + 2 * kHid + e] = params[L.valW + e];
+    }
+    if (tid < 2) {
+        lds[oHead + 3 * kHid + tid] = params[L.actb + tid];
+        lds[oHead + 3 * kHid + 3 + tid] = params[L.logstd + tid];
+    }
+    if (tid == 0) lds[oHead + 3 * kHid + 2] = params[L.valb];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, h = lane >> 5;
+    const int waves_per_block = blockDim.x >> 6;
+    const int64_t ntiles = (B + 31) / 32;
+    const float ls_h = lds[oHead + 3 * kHid + 3 + h];
+    const float std_h = expf(ls_h);
+    const float ba_h = lds[oHead + 3 * kHid + h];
+    const float ba_o = lds[oHead + 3 * kHid + (h ^ 1)];
+    const float bv = lds[oHead + 3 * kHid + 2];
+    const float log_scale = logf(std_h);
+    const float half_log_2pi = 0.918938533204672742f;  // log(sqrt(2*pi))
+
+    for (int64_t tile = (int64_t)blockIdx.x * waves_per_block + (tid >> 6); tile < ntiles;
+         tile += (int64_t)gridDim.x * waves_per_block) {
+        const int64_t row = tile * 32 + j;
+        const bool valid = row < B;
+        float o[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int col = 2 * s + h;
+            o[s] = (valid && col < D) ? obs[row * D + col] : 0.0f;
+        }
+        float head[3] = {0.f, 0.f, 0.f};  // mu0, mu1 partials (actor), value partial (critic)
+#pragma unroll 1
+        for (int net = 0; net < 2; ++net) {
+            f32x16 a0, a1;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                a0[reg] = lds[oB1 + net * kHid + rho(reg, h)];
+                a1[reg] = lds[oB1 + net * kHid + 32 + rho(reg, h)];
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (2 * s >= D) break;
+                a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + ((net * 2 + 0) * 4 + s) * 64 + lane],
+                                                          o[s], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + ((net * 2 + 1) * 4 + s) * 64 + lane],
+                                                          o[s], a1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                a0[reg] = tanh_f(a0[reg]);
+                a1[reg] = tanh_f(a1[reg]);
+            }
+            f32x16 c0, c1;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                c0[reg] = lds[oB2 + net * kHid + rho(reg, h)];
+                c1[reg] = lds[oB2 + net * kHid + 32 + rho(reg, h)];
+            }
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const f32x4 w0 = *reinterpret_cast<const f32x4 *>(
+                        &lds[oW2 + ((((net * 2 + 0) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+                    const f32x4 w1 = *reinterpret_cast<const f32x4 *>(
+                        &lds[oW2 + ((((net * 2 + 1) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float b = kt == 0 ? a0[4 * r4 + q] : a1[4 * r4 + q];
+                        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[q], b, c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[q], b, c1, 0, 0, 0);
+                    }
+                }
+            }
+            // heads over this lane's 32 hidden rows (ot = 0, 1; reg order), fma chain
+            if (net == 0) {
+                float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+                for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const float hv = tanh_f(ot ? c1[reg] : c0[reg]);
+                        const int idx = 32 * ot + rho(reg, h);
+                        p0 = __builtin_fmaf(lds[oHead + idx], hv, p0);
+                        p1 = __builtin_fmaf(lds[oHead + kHid + idx], hv, p1);
+                    }
+                }
+                head[0] = p0;
+                head[1] = p1;
+            } else {
+                float pv = 0.f;
+#pragma unroll
+                for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const float hv = tanh_f(ot ? c1[reg] : c0[reg]);
+                        pv = __builtin_fmaf(lds[oHead + 2 * kHid + 32 * ot + rho(reg, h)], hv, pv);
+                    }
+                }
+                head[2] = pv;
+            }
+        }
+        // join the two lane halves in a fixed order (half 0 + half 1), add biases
+        float full[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const float other = __shfl_xor(head[m], 32, 64);
+            full[m] = h == 0 ? head[m] + other : other + head[m];
+        }
+        const float mu_h = (h == 0 ? full[0] : full[1]) + ba_h;
+        const float mu_o = (h == 0 ? full[1] : full[0]) + ba_o;
+        (void)mu_o;
+        const float value = full[2] + bv;
+        float a_h = mu_h;
+        if (!deterministic) {
+            const uint4 r = philox_p(make_uint4((uint32_t)row, (uint32_t)((uint64_t)row >> 32),
+                                                (uint32_t)offset, (uint32_t)(offset >> 32)),
+                                     (uint32_t)seed, (uint32_t)(seed >> 32));
+            const float u1 = (float)((r.x >> 8) + 1u) * 0x1.0p-24f;  // (0, 1]
+            const float u2 = (float)(r.y >> 8) * 0x1.0p-24f;          // [0, 1)
+            const float rad = sqrtf(-2.0f * logf(u1));
+            float sn, cs;
+            sincosf(6.28318530717958648f * u2, &sn, &cs);
+            const float eps = h == 0 ? rad * cs : rad * sn;
+            a_h = mu_h + std_h * eps;
+        }
+        // Normal(mu, std).log_prob(a) summed over the 2 action dims
+        const float var = std_h * std_h;
+        const float d = a_h - mu_h;
+        const float lp_h = -(d * d) / (2.0f * var) - log_scale - half_log_2pi;
+        const float lp_o = __shfl_xor(lp_h, 32, 64);
+        const float logp = h == 0 ? lp_h + lp_o : lp_o + lp_h;
+        if (valid) {
+            if (mu_out) mu_out[row * 2 + h] = mu_h;
+            if (act_out) act_out[row * 2 + h] = a_h;
+            if (clip_out) clip_out[row * 2 + h] = a_h < -1.0f ? -1.0f : (a_h > 1.0f ? 1.0f : a_h);
+            if (h == 0) {
+                if (value_out) value_out[row] = value;
+                if (logp_out) logp_out[row] = logp;
+            }
+        }
+    }
+}
+
+hipError_t launch_policy_forward(const float *params, int32_t D, const float *obs, int64_t B,
+                                 float *mu, float *value, float *action, float *logp,
+                                 float *clipped, uint64_t seed, uint64_t offset,
+                                 int32_t deterministic, hipStream_t st) {
+    const int64_t tiles = (B + 31) / 32;
+    int64_t blocks = (tiles + 3) / 4;
+    const int64_t cap = 256 * 4;  // persistent: up to 4 workgroups (16 waves) per CU
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_policy, dim3((unsigned)blocks), dim3(256), 0, st, params, D, obs, B, mu,
+                       value, action, logp, clipped, seed, offset, deterministic);
+    return hipGetLastError();
 }
 
 }  // namespace fenvk

@@ -1,0 +1,153 @@
+"""Actor-critic MLP policy (SB3 ``MlpPolicy`` for a Box action space) on the gfx950 matrix cores.
+
+The reference trains ``PPO('MlpPolicy', env, n_steps=10, learning_rate=1e-3, ent_coef=0.01)``
+(vectorized_env.py:126-131) and plays back with ``model.predict(obs, deterministic=True)``
+(visualize_policy.py:16).  :class:`MlpPolicy` keeps SB3's parameter names (``state_dict`` /
+``load_state_dict`` interoperate with an SB3 ``policy.pth``) and runs the forward pass --
+both networks, Gaussian sampling, log-prob and action clipping -- in one HIP kernel
+(``policy_forward`` in include/fenv.h).  Parameters live in one flat fp32 device buffer.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+HID = 64
+
+# SB3 state_dict names and shapes, in the flat-buffer order of include/fenv.h
+PARAM_SPECS = [
+    ("mlp_extractor.policy_net.0.weight", (HID, "D")),
+    ("mlp_extractor.policy_net.0.bias", (HID,)),
+    ("mlp_extractor.policy_net.2.weight", (HID, HID)),
+    ("mlp_extractor.policy_net.2.bias", (HID,)),
+    ("mlp_extractor.value_net.0.weight", (HID, "D")),
+    ("mlp_extractor.value_net.0.bias", (HID,)),
+    ("mlp_extractor.value_net.2.weight", (HID, HID)),
+    ("mlp_extractor.value_net.2.bias", (HID,)),
+    ("action_net.weight", (2, HID)),
+    ("action_net.bias", (2,)),
+    ("value_net.weight", (1, HID)),
+    ("value_net.bias", (1,)),
+    ("log_std", (2,)),
+]
+
+
+def _shape(shp, D):
+    return tuple(D if s == "D" else s for s in shp)
+
+
+class MlpPolicy:
+    """Flat-parameter actor-critic with SB3 naming; forward on the HIP kernel."""
+
+    def __init__(self, obs_dim: int = 8, device=None, seed: int = 0, log_std_init: float = 0.0):
+        if obs_dim not in (6, 8):
+            raise ValueError("obs_dim must be 6 or 8 (vectorized_env.py:28-31)")
+        self.obs_dim = obs_dim
+        self.device = _lib.require_device(device)
+        n = int(_lib.lib().policy_param_count(obs_dim))
+        self.flat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self._views = {}
+        o = 0
+        for k, shp in PARAM_SPECS:
+            s = _shape(shp, obs_dim)
+            m = int(np.prod(s))
+            self._views[k] = self.flat[o:o + m].view(s)
+            o += m
+        assert o == n
+        self.reset_parameters(seed, log_std_init)
+        self._offset = 0
+        self.sample_seed = int(seed)
+
+    # ---------------------------------------------------------------- parameters
+    def reset_parameters(self, seed: int = 0, log_std_init: float = 0.0) -> None:
+        """SB3's init: orthogonal weights (gain sqrt(2) hidden, 0.01 action head, 1 value head),
+        zero biases, log_std = log_std_init (SB3 default 0.0; note vectorized_env.py:133 sets
+        log_std_init after construction, which SB3 ignores)."""
+        g = torch.Generator().manual_seed(seed)
+        for k, v in self._views.items():
+            if k.endswith("weight"):
+                gain = (0.01 if k.startswith("action_net")
+                        else 1.0 if k.startswith("value_net") else math.sqrt(2))
+                w = torch.empty(tuple(v.shape))
+                torch.nn.init.orthogonal_(w, gain=gain, generator=g)
+                v.copy_(w)
+            elif k == "log_std":
+                v.fill_(log_std_init)
+            else:
+                v.zero_()
+
+    def state_dict(self) -> dict:
+        return {k: v.detach().clone().cpu() for k, v in self._views.items()}
+
+    def load_state_dict(self, sd: dict, strict: bool = True) -> None:
+        """Accepts an SB3 policy state_dict (extra keys such as features extractors ignored)."""
+        for k, v in self._views.items():
+            if k not in sd:
+                if strict:
+                    raise KeyError(f"missing parameter {k}")
+                continue
+            t = torch.as_tensor(sd[k], dtype=torch.float32)
+            if tuple(t.shape) != tuple(v.shape):
+                raise ValueError(f"{k}: shape {tuple(t.shape)} != {tuple(v.shape)}")
+            v.copy_(t)
+
+    def parameters_flat(self) -> torch.Tensor:
+        return self.flat
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, obs: torch.Tensor, deterministic: bool = False, out: dict | None = None,
+                seed: int | None = None, offset: int | None = None) -> dict:
+        """obs [B, D] float32 on the device -> dict(mu, value, action, log_prob, clipped).
+
+        ``action`` is the unclipped sample (what SB3 stores in the rollout buffer); ``clipped``
+        is what collect_rollouts passes to env.step.  Each call advances the noise offset."""
+        if obs.dim() != 2 or obs.shape[1] != self.obs_dim:
+            raise ValueError(f"obs must be [B, {self.obs_dim}]")
+        if obs.dtype != torch.float32 or obs.device != self.device:
+            raise TypeError(f"obs must be float32 on {self.device}")
+        obs = obs.contiguous()
+        B = obs.shape[0]
+        dev = self.device
+        if out is None:
+            out = dict(mu=torch.empty((B, 2), device=dev), value=torch.empty(B, device=dev),
+                       action=torch.empty((B, 2), device=dev), log_prob=torch.empty(B, device=dev),
+                       clipped=torch.empty((B, 2), device=dev))
+        if offset is None:
+            offset = self._offset
+            self._offset += 1
+        s = self.sample_seed if seed is None else seed
+        _lib.check(_lib.lib().policy_forward(
+            _lib.ptr(self.flat), self.obs_dim, _lib.ptr(obs), B, _lib.ptr(out.get("mu")),
+            _lib.ptr(out.get("value")), _lib.ptr(out.get("action")), _lib.ptr(out.get("log_prob")),
+            _lib.ptr(out.get("clipped")), int(s) & 0xFFFFFFFFFFFFFFFF, int(offset),
+            int(bool(deterministic)), _lib.current_stream(dev)), "policy_forward")
+        return out
+
+    __call__ = forward
+
+    def predict(self, observation, deterministic: bool = True):
+        """SB3 ``predict``: numpy obs [B, D] -> (clipped actions numpy [B, 2], None)."""
+        obs = torch.as_tensor(np.asarray(observation, np.float32)).to(self.device)
+        r = self.forward(obs, deterministic=deterministic)
+        return r["clipped"].cpu().numpy(), None
+
+
+def smoke_check(device="cuda:0") -> None:
+    """Small forward vs the torch-CPU restatement (oracle/policy_oracle.py)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    import policy_oracle as po
+    pol = MlpPolicy(8, device=device, seed=3)
+    g = torch.Generator().manual_seed(0)
+    obs = torch.rand((77, 8), generator=g) * 2 - 1
+    r = pol.forward(obs.to(device), deterministic=True)
+    mu, val = po.forward({k: v for k, v in pol.state_dict().items()}, obs)
+    torch.cuda.synchronize()
+    assert torch.allclose(r["mu"].cpu(), mu, rtol=1e-4, atol=1e-5), "policy mu mismatch"
+    assert torch.allclose(r["value"].cpu(), val, rtol=1e-4, atol=1e-5), "policy value mismatch"

@@ -106,7 +106,7 @@ class FormationEnv:
             seed = cfg.get("seed", None)
         if seed is None:  # the torch global stream the reference draws from (simulate.py:133)
             seed = torch.initial_seed()
-        self.seed = int(seed) & 0xFFFFFFFF
+        self.rng_seed = int(seed) & 0xFFFFFFFF
         mode = reset_mode or cfg.get("reset_mode", "mt19937")
         if mode not in _lib.RESET_MODES:
             raise ValueError(f"reset_mode must be one of {sorted(_lib.RESET_MODES)}")
@@ -123,7 +123,7 @@ class FormationEnv:
         with torch.cuda.device(self.device):
             _lib.check(L.fenv_create(ctypes.byref(h), self.device.index, self.num_formation,
                                      self.num_agents_per_formation, int(self.goal_in_obs),
-                                     self.share_reward_ratio, self.max_steps, self.seed,
+                                     self.share_reward_ratio, self.max_steps, self.rng_seed,
                                      _lib.RESET_MODES[mode], self.first_formation,
                                      self.total_formations), "fenv_create")
         self._h = h

@@ -182,8 +182,8 @@ def test_philox_mode(venv):
     env = make_env(venv, F, N, True, 5, reset_mode="philox", max_steps=5,
                    first_formation=300, total_formations=total)
     full = make_env(venv, total, N, True, 5, reset_mode="philox", max_steps=5)
-    o = env.reset()
-    of = full.reset()
+    o = env.reset().copy()      # numpy results alias env buffers (reference Q9)
+    of = full.reset().copy()
     assert np.array_equal(bits(o), bits(of[300 * N:600 * N]))   # sharding invariance
     px, py, gx, gy, t = (v.cpu().numpy() for v in env.get_state())
     assert px.min() >= 0 and px.max() < 400 and py.min() >= 0 and py.max() < 100

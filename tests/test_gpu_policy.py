@@ -1,0 +1,113 @@
+"""GPU parity of the policy forward (policy_forward, MFMA kernel) against the torch-CPU fp32
+restatement of SB3's ActorCriticPolicy (oracle/policy_oracle.py; parity unpinned vs SB3 itself,
+which is not installed).  Tolerance: |err| <= 2e-5 + 2e-5 * |ref| (fp32, different summation
+order and tanh implementation)."""
+import numpy as np
+import pytest
+import torch
+
+import policy_oracle as po
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+ATOL, RTOL = 2e-5, 2e-5
+
+
+@pytest.fixture(scope="module")
+def pol_mod(pkg):
+    from importlib import import_module
+    return import_module(pkg.__name__ + ".policy")
+
+
+def randomize(pol, seed):
+    g = torch.Generator().manual_seed(seed)
+    sd = pol.state_dict()
+    for k, v in sd.items():
+        if k.endswith("bias"):
+            sd[k] = torch.randn(v.shape, generator=g) * 0.3
+        elif k == "log_std":
+            sd[k] = torch.randn(v.shape, generator=g) * 0.5
+        else:
+            sd[k] = v + torch.randn(v.shape, generator=g) * 0.05
+    pol.load_state_dict(sd)
+    return sd
+
+
+@pytest.mark.parametrize("D", [8, 6])
+@pytest.mark.parametrize("B", [1, 31, 32, 33, 1000, 65543])
+def test_deterministic_forward(pol_mod, D, B):
+    pol = pol_mod.MlpPolicy(D, device=DEV, seed=B)
+    sd = randomize(pol, B + D)
+    g = torch.Generator().manual_seed(B)
+    obs = (torch.rand((B, D), generator=g) * 2.4 - 1.2)
+    r = pol.forward(obs.to(DEV), deterministic=True)
+    mu, val = po.forward(sd, obs)
+    torch.testing.assert_close(r["mu"].cpu(), mu, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["value"].cpu(), val, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["action"].cpu(), mu, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["clipped"].cpu(), mu.clamp(-1, 1), atol=ATOL, rtol=RTOL)
+    lp = po.log_prob(sd, mu, mu)
+    torch.testing.assert_close(r["log_prob"].cpu(), lp, atol=ATOL, rtol=RTOL)
+
+
+def test_large_preactivations(pol_mod):
+    """Saturating tanh inputs (|x| >> 1) and tiny ones (|x| < 0.3, the polynomial branch)."""
+    pol = pol_mod.MlpPolicy(8, device=DEV, seed=1)
+    sd = randomize(pol, 9)
+    for scale in (1e-4, 0.05, 3.0, 40.0):
+        obs = (torch.rand((4096, 8), generator=torch.Generator().manual_seed(2)) * 2 - 1) * scale
+        r = pol.forward(obs.to(DEV), deterministic=True)
+        mu, val = po.forward(sd, obs)
+        torch.testing.assert_close(r["mu"].cpu(), mu, atol=ATOL, rtol=RTOL)
+        torch.testing.assert_close(r["value"].cpu(), val, atol=ATOL, rtol=RTOL)
+
+
+def test_stochastic_sample_and_log_prob(pol_mod):
+    B, seed, off = 50000, 77, 5
+    pol = pol_mod.MlpPolicy(8, device=DEV, seed=4)
+    sd = randomize(pol, 4)
+    obs = torch.rand((B, 8), generator=torch.Generator().manual_seed(3)) * 2 - 1
+    r = pol.forward(obs.to(DEV), deterministic=False, seed=seed, offset=off)
+    mu, _ = po.forward(sd, obs)
+    eps = torch.from_numpy(po.philox_normals(B, seed, off)).float()
+    std = sd["log_std"].exp()
+    a = mu + std * eps
+    torch.testing.assert_close(r["action"].cpu(), a, atol=5e-5, rtol=5e-5)
+    act = r["action"].cpu()
+    torch.testing.assert_close(r["log_prob"].cpu(), po.log_prob(sd, r["mu"].cpu(), act),
+                               atol=1e-4, rtol=1e-5)
+    torch.testing.assert_close(r["clipped"].cpu(), act.clamp(-1, 1), atol=0, rtol=0)
+    # the noise is standard normal
+    e = ((act - r["mu"].cpu()) / std).numpy()
+    assert abs(e.mean()) < 0.02 and abs(e.std() - 1) < 0.02
+    # offset advances the stream; same (seed, offset) reproduces it
+    r2 = pol.forward(obs.to(DEV), deterministic=False, seed=seed, offset=off)
+    assert torch.equal(r2["action"], r["action"])
+    r3 = pol.forward(obs.to(DEV), deterministic=False, seed=seed, offset=off + 1)
+    assert not torch.equal(r3["action"], r["action"])
+
+
+def test_state_dict_names_roundtrip(pol_mod):
+    pol = pol_mod.MlpPolicy(8, device=DEV)
+    sd = pol.state_dict()
+    assert list(sd) == [k for k, _ in po.SB3_KEYS]
+    assert sum(v.numel() for v in sd.values()) == 9669
+    sd2 = {k: v + 1 for k, v in sd.items()}
+    pol.load_state_dict(sd2)
+    for k, v in pol.state_dict().items():
+        assert torch.equal(v, sd2[k])
+    with pytest.raises(KeyError):
+        pol.load_state_dict({})
+
+
+def test_policy_on_env_observations(pol_mod, venv):
+    env = venv.FormationEnv({"num_formation": 512, "num_agents_per_formation": 10,
+                             "goal_in_obs": True}, device=DEV, seed=2)
+    obs = env.reset_tensor()
+    pol = pol_mod.MlpPolicy(8, device=DEV, seed=0)
+    r = pol.forward(obs, deterministic=True)
+    mu, val = po.forward(pol.state_dict(), obs.cpu())
+    torch.testing.assert_close(r["mu"].cpu(), mu, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["value"].cpu(), val, atol=ATOL, rtol=RTOL)
+    acts, _ = pol.predict(obs.cpu().numpy())
+    assert acts.shape == (5120, 2) and np.all(np.abs(acts) <= 1)
