@@ -140,6 +140,7 @@ def main():
         if not args.no_stats:
             side.wait_stream(main)
             with torch.cuda.stream(side):
+                stats.reserve()
                 env.reduce_partials(partials[s], reds[s])
                 stats.submit(reds[s])
                 released[s] = torch.cuda.Event()

@@ -272,23 +272,37 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         s.ep = st.ep[f];
     }
     bool any_reset = false;
-    float2 an = active ? act[a] : make_float2(0.f, 0.f);
-    for (int32_t k = 0; k < T; ++k) {
-        const float2 ac = an;
-        if (active && k + 1 < T) an = act[(int64_t)(k + 1) * A + a];  // prefetch next step
-        float rw;
-        bool dn, rs;
-        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
-        any_reset |= rs;
-        const int64_t row = (int64_t)k * A + a;
-        float o[8];
-        env_obs<D>(x, s, o);
-        if (obs) store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-        if (active) {
-            if (rew) rew[row] = rw;
-            if (done) done[row] = (uint8_t)dn;
-            rsum += rw;
-            dsum += dn ? 1.0f : 0.0f;
+    // Rolling action prefetch: a ring of kPF registers keeps the loads of the next kPF steps in
+    // flight while a step computes (kPF = 1: load step k+1 during step k).
+#ifndef FENV_ACT_PREFETCH
+#define FENV_ACT_PREFETCH 1
+#endif
+    constexpr int kPF = FENV_ACT_PREFETCH;
+    float2 ring[kPF];
+#pragma unroll
+    for (int j = 0; j < kPF; ++j)
+        ring[j] = (active && j < T) ? act[(int64_t)j * A + a] : make_float2(0.f, 0.f);
+    for (int32_t k0 = 0; k0 < T; k0 += kPF) {
+#pragma unroll
+        for (int j = 0; j < kPF; ++j) {
+            const int32_t k = k0 + j;
+            if (k >= T) break;
+            const float2 ac = ring[j];
+            if (active && k + kPF < T) ring[j] = act[(int64_t)(k + kPF) * A + a];
+            float rw;
+            bool dn, rs;
+            env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+            any_reset |= rs;
+            const int64_t row = (int64_t)k * A + a;
+            float o[8];
+            env_obs<D>(x, s, o);
+            if (obs) store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
+            if (active) {
+                if (rew) rew[row] = rw;
+                if (done) done[row] = (uint8_t)dn;
+                rsum += rw;
+                dsum += dn ? 1.0f : 0.0f;
+            }
         }
     }
     if (active) {

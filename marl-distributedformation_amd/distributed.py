@@ -39,35 +39,42 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
 
 
 class StatsReducer:
-    """Double-buffered, stream-overlapped all-reduce of a small stats vector.
+    """Stream-overlapped all-reduce of a small stats vector, two submissions in flight.
 
-    ``submit(v)`` copies v into the next slot and starts an async all-reduce on a side stream
-    (after the producing stream's work); the main stream never waits on the collective except
-    when a slot is reused two submissions later.  ``result()`` waits and returns the last sum.
-    With world_size 1 it degenerates to a copy."""
+    ``submit(v)`` starts an async all-reduce of ``v`` IN PLACE on a side stream (after the
+    current stream's work that produced v); the caller alternates two buffers and must not
+    overwrite a buffer until the submission two calls later (``submit`` then waits for the
+    collective that used the same slot).  ``result()`` waits and returns the last buffer.
+    With world_size 1 there is nothing to reduce and ``v`` is returned as is."""
 
-    def __init__(self, n: int, device, dtype=torch.float64):
+    def __init__(self, n: int, device):
         self.device = torch.device(device)
-        self.buf = [torch.zeros(n, dtype=dtype, device=self.device) for _ in range(2)]
         self.work = [None, None]
+        self.bufs = [None, None]
         self.k = 0
         self.cuda = self.device.type == "cuda"
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
         self.dist = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
-    def submit(self, v: torch.Tensor) -> None:
+    def reserve(self) -> None:
+        """Make the current stream wait until the next slot's previous all-reduce finished
+        (call before overwriting the buffer you are about to submit)."""
         s = self.k % 2
         if self.work[s] is not None:
             self.work[s].wait()
             self.work[s] = None
-        self.buf[s].copy_(v)
+
+    def submit(self, v: torch.Tensor) -> None:
+        self.reserve()
+        s = self.k % 2
+        self.bufs[s] = v
         if self.dist:
             if self.cuda:
                 self.side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self.side):
-                    self.work[s] = dist.all_reduce(self.buf[s], async_op=True)
+                    self.work[s] = dist.all_reduce(v, async_op=True)
             else:
-                self.work[s] = dist.all_reduce(self.buf[s], async_op=True)
+                self.work[s] = dist.all_reduce(v, async_op=True)
         self.k += 1
 
     def result(self) -> torch.Tensor:
@@ -77,7 +84,7 @@ class StatsReducer:
             self.work[s] = None
         if self.cuda:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
-        return self.buf[s]
+        return self.bufs[s]
 
 
 def max_over_ranks(x: float, device=None) -> float:

@@ -105,6 +105,61 @@ __global__ __launch_bounds__(256) void k_pattern_lds(const float2 *__restrict__ 
     }
 }
 
+
+// explore: PFALL = prefetch all T action loads at entry; TWO = each lane owns 2 agents (2 groups
+// of 60 in one wave); PERSIST = grid of 256*8 blocks striding over wave tiles.
+template <bool PFALL, bool TWO, bool PERSIST>
+__global__ __launch_bounds__(256) void k_explore(const float2 *__restrict__ act, float *__restrict__ obs,
+                                                 float *__restrict__ rew, unsigned char *__restrict__ done,
+                                                 long A, int T, long ntiles) {
+    __shared__ __attribute__((aligned(16))) float stage[4][64 * 8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float *st = stage[w];
+    const long wstride = PERSIST ? (long)gridDim.x * 4 : 0;
+    for (long tile = (long)blockIdx.x * 4 + w; tile < ntiles; tile += (PERSIST ? wstride : ntiles)) {
+        constexpr int G = TWO ? 2 : 1;
+        long a0[G]; bool active[G]; float acc[G]; float2 an[G];
+        float2 pre[16];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            a0[g] = (tile * G + g) * 60;
+            active[g] = lane < 60 && a0[g] + lane < A;
+            acc[g] = 0.f;
+            an[g] = active[g] ? act[a0[g] + lane] : make_float2(0, 0);
+        }
+        if (PFALL) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) pre[k] = (k < T && active[0]) ? act[(long)k * A + a0[0] + lane] : make_float2(0, 0);
+        }
+        for (int k = 0; k < T; ++k) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float2 ac = an[g];
+                if (PFALL && g == 0) {
+                    ac = make_float2(0, 0);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) if (q == k) ac = pre[q];
+                } else if (active[g] && k + 1 < T) an[g] = act[(long)(k + 1) * A + a0[g] + lane];
+                acc[g] += ac.x * 0.5f + ac.y;
+                const long row0 = (long)k * A + a0[g];
+                v4f o0 = {acc[g], ac.x, ac.y, 1.f}, o1 = {ac.y, acc[g], 2.f, 3.f};
+                *reinterpret_cast<v4f *>(&st[lane * 8]) = o0;
+                *reinterpret_cast<v4f *>(&st[lane * 8 + 4]) = o1;
+                __builtin_amdgcn_wave_barrier();
+                v4f *ob = reinterpret_cast<v4f *>(obs + row0 * 8);
+                v4f q0 = *reinterpret_cast<v4f *>(&st[lane * 4]);
+                v4f q1 = *reinterpret_cast<v4f *>(&st[(lane + 64) * 4]);
+                const long left = A - a0[g];
+                const int nq = 2 * (int)(left <= 0 ? 0 : (left < 60 ? left : 60));
+                if (lane < nq) ob[lane] = q0;
+                if (lane + 64 < nq) ob[lane + 64] = q1;
+                if (active[g]) { rew[row0 + lane] = acc[g]; done[row0 + lane] = (unsigned char)(acc[g] > 0.f); }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+}
+
 template <class F>
 float timeit(F f, int reps) {
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
@@ -141,5 +196,11 @@ int main() {
 #define RUNL(NT, PD) { float ms = timeit([&] { hipLaunchKernelGGL((k_pattern_lds<NT, PD>), dim3(blocks), dim3(256), 0, 0, act, obs, rew, done, A, T); }, 20); \
         printf("lds-transpose nt=%d packdone=%d  %.3f ms  %.1f GB/s\n", NT, PD, ms, algo / ms / 1e6); }
     RUNL(false, false) RUNL(true, false) RUNL(false, true) RUNL(true, true)
+#define RUNX(PF, TW, PE, NB) { const long nt = (waves + (TW ? 1 : 0)) / (TW ? 2 : 1); unsigned nb = PE ? NB : (unsigned)((nt + 3) / 4); \
+        float ms = timeit([&] { hipLaunchKernelGGL((k_explore<PF, TW, PE>), dim3(nb), dim3(256), 0, 0, act, obs, rew, done, A, T, nt); }, 20); \
+        printf("explore pfall=%d two=%d persist=%d blocks=%u  %.3f ms  %.1f GB/s\n", PF, TW, PE, nb, ms, algo / ms / 1e6); }
+    RUNX(false, false, false, 0) RUNX(true, false, false, 0) RUNX(false, true, false, 0)
+    RUNX(false, false, true, 2048) RUNX(false, false, true, 4096) RUNX(false, false, true, 8192)
+    RUNX(true, false, true, 2048) RUNX(false, true, true, 2048)
     return 0;
 }
