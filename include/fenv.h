@@ -81,12 +81,12 @@ int fenv_step(fenv_t *env, const float *act, float *obs, float *rew, uint8_t *do
 
 /* T consecutive env.step calls fused in one launch (state kept on chip): act [T][A][2],
  * obs [T][A][D] (obs[k] = observation returned by step k), rew [T][A], done [T][A].
- * Bit-identical to T fenv_step calls.  partial (may be NULL) receives per-wavefront
- * {sum reward, sum done} pairs for fenv_reduce_partials. */
+ * Bit-identical to T fenv_step calls.  partial (may be NULL) receives one {sum reward,
+ * sum done} float pair per workgroup (fenv_partial_count of them) for fenv_reduce_partials. */
 int fenv_rollout(fenv_t *env, int32_t T, const float *act, float *obs, float *rew,
                  uint8_t *done, float *partial, void *stream);
 
-/* Number of float2 partial records fenv_rollout writes (one per wavefront/workgroup). */
+/* Number of float2 partial records fenv_rollout writes (one per workgroup). */
 int64_t fenv_partial_count(const fenv_t *env);
 
 /* Deterministic fixed-order reduction of `count` partial records into out[2] (double, device):
@@ -114,6 +114,10 @@ int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64
                           int64_t count, int32_t num_agents, float *px_host, float *py_host,
                           float *gx_host, float *gy_host);
 
+/* Diagnostic: one of the kernels' fp32 primitives over n device inputs (op 0: a/400,
+ * 1: a/600, 2: sqrtf(a), 3: sqrtf(fmaf(b, b, a*a))) into out; for parity tests. */
+int fenv_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n, void *stream);
+
 /* Host-only: the fp32 desired neighbour distance the reference uses (simulate.py:26). */
 float fenv_desired_neighbor_dist(int32_t num_agents);
 
@@ -123,7 +127,7 @@ float fenv_desired_neighbor_dist(int32_t num_agents);
  * mu + exp(log_std) * eps, log_prob = sum_j Normal(mu_j, exp(log_std_j)).log_prob(action_j),
  * clipped = clamp(action, -1, 1) (what collect_rollouts hands to env.step).
  *
- * params: flat f32 buffer (device) in the order of policy_param_layout():
+ * params: flat f32 buffer (device), SB3 state_dict order (policy_param_count floats):
  *   pi0.W[64][D] pi0.b[64] pi2.W[64][64] pi2.b[64] vf0.W[64][D] vf0.b[64] vf2.W[64][64]
  *   vf2.b[64] act.W[2][64] act.b[2] val.W[1][64] val.b[1] log_std[2]
  * obs [B][D]; outputs (each may be NULL): mu [B][2], value [B], action [B][2] (unclipped
@@ -133,6 +137,14 @@ int policy_param_count(int32_t obs_dim);
 int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B,
                    float *mu, float *value, float *action, float *logp, float *clipped,
                    uint64_t seed, uint64_t offset, int32_t deterministic, void *stream);
+
+/* SB3 RolloutBuffer.compute_returns_and_advantage (GAE) over [T][A] device buffers:
+ * rew, values f32, episode_starts u8 (1 where step k began an episode), last_values [A] f32
+ * (value of the observation after the last step), last_dones [A] u8.  Writes advantages and
+ * returns (= advantages + values), [T][A] f32. */
+int rollout_gae(const float *rew, const float *values, const uint8_t *episode_starts,
+                const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
+                float gamma, float gae_lambda, float *advantages, float *returns, void *stream);
 
 const char *fenv_last_error(void);
 

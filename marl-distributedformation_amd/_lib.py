@@ -48,6 +48,8 @@ SIGNATURES = {
     "fenv_fp_probe": (_I32, [_I32, _P, _P, _P, _I64, _P]),
     "policy_param_count": (_I32, [_I32]),
     "policy_forward": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _U64, _U64, _I32, _P]),
+    "rollout_gae": (_I32, [_P, _P, _P, _P, _P, _I32, _I64, ctypes.c_float, ctypes.c_float, _P, _P,
+                           _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
 

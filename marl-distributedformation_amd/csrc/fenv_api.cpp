@@ -370,4 +370,15 @@ int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64
     return FENV_OK;
 }
 
+int rollout_gae(const float *rew, const float *values, const uint8_t *episode_starts,
+                const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
+                float gamma, float gae_lambda, float *advantages, float *returns, void *stream) {
+    if (!rew || !values || !episode_starts || !last_values || !last_dones || !advantages ||
+        !returns || T < 1 || A < 1)
+        return fail(FENV_EINVAL, "rollout_gae: bad arguments");
+    FENV_HIP(fenvk::launch_gae(rew, values, episode_starts, last_values, last_dones, T, A, gamma,
+                               gae_lambda, advantages, returns, as_stream(stream)));
+    return FENV_OK;
+}
+
 }  // extern "C"

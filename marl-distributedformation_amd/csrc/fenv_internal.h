@@ -55,4 +55,8 @@ hipError_t launch_policy_forward(const float *params, int32_t D, const float *ob
                                  float *clipped, uint64_t seed, uint64_t offset,
                                  int32_t deterministic, hipStream_t st);
 
+hipError_t launch_gae(const float *rew, const float *values, const uint8_t *episode_starts,
+                      const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
+                      float gamma, float lam, float *adv, float *ret, hipStream_t st);
+
 }  // namespace fenvk

@@ -280,3 +280,42 @@ hipError_t launch_policy_forward(const float *params, int32_t D, const float *ob
 }
 
 }  // namespace fenvk
+
+namespace fenvk {
+
+// SB3 RolloutBuffer.compute_returns_and_advantage (GAE(lambda)), one lane per env column,
+// backwards over the T steps of the [T][A] buffers.  Elementwise/HBM-bound: per agent-step
+// reads reward, value, episode_start (4+4+1 B) and writes advantage, return (8 B).
+__global__ __launch_bounds__(256) void k_gae(const float *__restrict__ rew,
+                                             const float *__restrict__ values,
+                                             const uint8_t *__restrict__ episode_starts,
+                                             const float *__restrict__ last_values,
+                                             const uint8_t *__restrict__ last_dones, int32_t T,
+                                             int64_t A, float gamma, float lam,
+                                             float *__restrict__ adv, float *__restrict__ ret) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= A) return;
+    float last = 0.0f;
+    float next_v = last_values[a];
+    float next_nt = 1.0f - (float)last_dones[a];
+    for (int32_t k = T - 1; k >= 0; --k) {
+        const int64_t r = (int64_t)k * A + a;
+        const float v = values[r];
+        const float delta = rew[r] + gamma * next_v * next_nt - v;
+        last = delta + gamma * lam * next_nt * last;
+        adv[r] = last;
+        ret[r] = last + v;
+        next_v = v;
+        next_nt = 1.0f - (float)episode_starts[r];
+    }
+}
+
+hipError_t launch_gae(const float *rew, const float *values, const uint8_t *episode_starts,
+                      const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
+                      float gamma, float lam, float *adv, float *ret, hipStream_t st) {
+    hipLaunchKernelGGL(k_gae, dim3((unsigned)((A + 255) / 256)), dim3(256), 0, st, rew, values,
+                       episode_starts, last_values, last_dones, T, A, gamma, lam, adv, ret);
+    return hipGetLastError();
+}
+
+}  // namespace fenvk

@@ -63,6 +63,10 @@ class MlpPolicy:
         self.sample_seed = int(seed)
 
     # ---------------------------------------------------------------- parameters
+    def param_shapes(self):
+        """[(SB3 name, shape)] in flat-buffer order."""
+        return [(k, _shape(shp, self.obs_dim)) for k, shp in PARAM_SPECS]
+
     def reset_parameters(self, seed: int = 0, log_std_init: float = 0.0) -> None:
         """SB3's init: orthogonal weights (gain sqrt(2) hidden, 0.01 action head, 1 value head),
         zero biases, log_std = log_std_init (SB3 default 0.0; note vectorized_env.py:133 sets

@@ -1,0 +1,124 @@
+"""Device-resident rollout collection (SB3 ``collect_rollouts`` + ``RolloutBuffer``) for PPO.
+
+The reference trains with ``PPO('MlpPolicy', env, n_steps=10, ...)`` (vectorized_env.py:126-134):
+every env step SB3 moves obs to the policy device, samples actions, clips them to the Box,
+calls ``env.step`` on numpy arrays and appends to host numpy buffers ``[n_steps, n_envs, .]``.
+Here the whole loop stays in HBM: :class:`RolloutBuffer` holds ``[T, A, .]`` device tensors, the
+policy forward (``policy_forward``) writes actions/values/log-probs straight into them, the env
+step (``fenv_step``) writes rewards/dones, and GAE runs in one kernel (``rollout_gae``).
+Semantics follow SB3 2.x ``OnPolicyAlgorithm.collect_rollouts`` / ``RolloutBuffer``: the buffer
+stores the obs the action was taken on, the UNCLIPPED action, ``episode_starts`` = the previous
+step's dones, and no timeout bootstrap (the reference's infos carry no ``TimeLimit`` keys).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+
+@dataclass
+class RolloutBatch:
+    observations: torch.Tensor
+    actions: torch.Tensor
+    old_values: torch.Tensor
+    old_log_prob: torch.Tensor
+    advantages: torch.Tensor
+    returns: torch.Tensor
+
+
+class RolloutBuffer:
+    """``[T, A, .]`` device buffers (SB3 RolloutBuffer fields)."""
+
+    def __init__(self, n_steps: int, n_envs: int, obs_dim: int, device, gamma: float = 0.99,
+                 gae_lambda: float = 0.95):
+        T, A, dev = int(n_steps), int(n_envs), torch.device(device)
+        self.n_steps, self.n_envs, self.obs_dim, self.device = T, A, obs_dim, dev
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.observations = torch.zeros((T, A, obs_dim), **f32)
+        self.actions = torch.zeros((T, A, 2), **f32)
+        self.clipped = torch.zeros((T, A, 2), **f32)
+        self.rewards = torch.zeros((T, A), **f32)
+        self.values = torch.zeros((T, A), **f32)
+        self.log_probs = torch.zeros((T, A), **f32)
+        self.mu = torch.zeros((T, A, 2), **f32)
+        self.episode_starts = torch.zeros((T, A), dtype=torch.bool, device=dev)
+        self.dones = torch.zeros((T, A), dtype=torch.bool, device=dev)
+        self.advantages = torch.zeros((T, A), **f32)
+        self.returns = torch.zeros((T, A), **f32)
+        self.pos = 0
+
+    def reset(self) -> None:
+        self.pos = 0
+
+    def full(self) -> bool:
+        return self.pos == self.n_steps
+
+    def compute_returns_and_advantage(self, last_values: torch.Tensor,
+                                      dones: torch.Tensor) -> None:
+        """SB3 RolloutBuffer.compute_returns_and_advantage (GAE), one HIP kernel."""
+        lv = last_values.contiguous().float()
+        ld = dones.contiguous().to(torch.bool)
+        _lib.check(_lib.lib().rollout_gae(
+            _lib.ptr(self.rewards), _lib.ptr(self.values), _lib.ptr(self.episode_starts),
+            _lib.ptr(lv), _lib.ptr(ld), self.n_steps, self.n_envs, self.gamma, self.gae_lambda,
+            _lib.ptr(self.advantages), _lib.ptr(self.returns), _lib.current_stream(self.device)),
+            "rollout_gae")
+
+    def get(self, batch_size: int | None, generator: torch.Generator | None = None):
+        """Shuffled minibatches over the flattened T*A samples (SB3 RolloutBuffer.get)."""
+        n = self.n_steps * self.n_envs
+        idx = torch.randperm(n, device=self.device, generator=generator)
+        bs = n if batch_size is None else int(batch_size)
+        obs = self.observations.reshape(n, self.obs_dim)
+        act = self.actions.reshape(n, 2)
+        val = self.values.reshape(n)
+        lp = self.log_probs.reshape(n)
+        adv = self.advantages.reshape(n)
+        ret = self.returns.reshape(n)
+        for s in range(0, n, bs):
+            j = idx[s:s + bs]
+            yield RolloutBatch(obs[j], act[j], val[j], lp[j], adv[j], ret[j])
+
+
+class RolloutCollector:
+    """SB3 ``collect_rollouts`` on device: policy forward + env step per step, no host copies."""
+
+    def __init__(self, env, policy, buffer: RolloutBuffer, seed: int = 0):
+        if buffer.n_envs != env.num_envs or buffer.obs_dim != env.obs_dim:
+            raise ValueError("buffer shape does not match the env")
+        self.env, self.policy, self.buffer = env, policy, buffer
+        self.seed = int(seed)
+        self.offset = 0
+        self.num_timesteps = 0
+        self.last_obs = env.reset_tensor().clone()
+        self.last_episode_starts = torch.ones(env.num_envs, dtype=torch.bool, device=env.device)
+        self._obs = torch.empty_like(self.last_obs)
+        self._rew = torch.empty(env.num_envs, dtype=torch.float32, device=env.device)
+        self._done = torch.empty(env.num_envs, dtype=torch.bool, device=env.device)
+        self._last_values = torch.empty(env.num_envs, dtype=torch.float32, device=env.device)
+
+    def collect(self, deterministic: bool = False) -> RolloutBuffer:
+        b = self.buffer
+        b.reset()
+        for k in range(b.n_steps):
+            b.observations[k].copy_(self.last_obs)
+            self.policy.forward(self.last_obs, deterministic=deterministic,
+                                out=dict(mu=b.mu[k], value=b.values[k], action=b.actions[k],
+                                         log_prob=b.log_probs[k], clipped=b.clipped[k]),
+                                seed=self.seed, offset=self.offset)
+            self.offset += 1
+            # the env is stepped with the clipped action (collect_rollouts np.clip)
+            self.env.step_tensor(b.clipped[k], obs=self._obs, rew=b.rewards[k], done=b.dones[k])
+            b.episode_starts[k].copy_(self.last_episode_starts)
+            self.last_obs.copy_(self._obs)
+            self.last_episode_starts.copy_(b.dones[k])
+            self.num_timesteps += self.env.num_envs
+            b.pos += 1
+        self.policy.forward(self.last_obs, deterministic=True, out=dict(value=self._last_values),
+                            seed=self.seed, offset=0)  # value of the final observation
+        b.compute_returns_and_advantage(self._last_values, self.last_episode_starts)
+        return b
