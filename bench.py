@@ -8,7 +8,7 @@ on 1, 2, 4 or 8 GPUs).  A "step" is one env step of every agent; steps run as fu
 `--chunk` steps per launch (SB3's n_steps=10 rollout, vectorized_env.py:128) writing obs /
 reward / done for every step into a device rollout buffer, with the actions read from HBM
 (inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
-over RCCL once per rollout on a side stream.
+over RCCL every --stats-every rollouts on a side stream.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -62,6 +62,50 @@ def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
                       f", 1 thread of {os.cpu_count()} host CPUs"}
 
 
+def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollouts: int) -> dict:
+    """Secondary measurement (BASELINE config 2): on-device PPO rollout collection with the MFMA
+    policy forward + env step per step (65536 formations x 10 agents), plus the policy
+    kernel's fp32-MFMA utilisation."""
+    import torch
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    pol_mod = import_module(pkgname + ".policy")
+    ro = import_module(pkgname + ".rollout")
+    cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=1, reset_mode="philox")
+    A = env.num_envs
+    pol = pol_mod.MlpPolicy(8, device=dev, seed=0)
+    buf = ro.RolloutBuffer(10, A, 8, dev)
+    col = ro.RolloutCollector(env, pol, buf, seed=0)
+    for _ in range(2):
+        col.collect()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(rollouts):
+        col.collect()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # policy kernel alone, HIP events on its stream
+    obs = buf.observations[0]
+    out = dict(mu=buf.mu[0], value=buf.values[0], action=buf.actions[0],
+               log_prob=buf.log_probs[0], clipped=buf.clipped[0])
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(20)]
+    for a, b in evs:
+        a.record()
+        pol.forward(obs, out=out, seed=0, offset=0)
+        b.record()
+    torch.cuda.synchronize()
+    pk_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    flop = 18816.0 * A
+    return {"workload": f"config2: {formations} formations x {agents} agents, PPO rollout "
+                        f"(n_steps=10): MFMA policy forward + env step per step, GAE",
+            "value": A * 10 * rollouts / el, "unit": "agent-steps/s",
+            "policy_kernel_ms": pk_ms, "policy_tflops": flop / (pk_ms * 1e-3) / 1e12,
+            "mfma_fp32_peak_tflops": 157.3,
+            "mfma_frac": flop / (pk_ms * 1e-3) / 1e12 / 157.3}
+
+
 def load_pmc_traffic(workload: str):
     """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -89,6 +133,13 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--event-group", type=int, default=5,
+                    help="HIP events bracket each run of this many consecutive rollout launches; "
+                         "avg launch duration = bracketed time / launches (includes the "
+                         "boundaries between them, so it is conservative)")
+    ap.add_argument("--stats-every", type=int, default=10,
+                    help="reduce + all-reduce the episode stats every this many rollouts")
+    ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
     args = ap.parse_args()
 
     import torch
@@ -128,16 +179,17 @@ def main():
     stats = pdist.StatsReducer(2, dev)
     env.reset_tensor()
 
-    def chunk(k, ev=None):
-        s = k % 2
-        if released[s] is not None:
+    def chunk(k, ev=None, ev_end=None):
+        stat = not args.no_stats and (k + 1) % args.stats_every == 0
+        s = (k // args.stats_every) % 2
+        if stat and released[s] is not None:
             main.wait_event(released[s])
         if ev is not None:
             ev[0].record(main)
-        env.rollout(acts[k % 2], obs, rew, done, partial=None if args.no_stats else partials[s])
-        if ev is not None:
-            ev[1].record(main)
-        if not args.no_stats:
+        env.rollout(acts[k % 2], obs, rew, done, partial=partials[s] if stat else None)
+        if ev_end is not None:
+            ev_end.record(main)
+        if stat:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 stats.reserve()
@@ -147,7 +199,7 @@ def main():
                 released[s].record(side)
 
     warm_chunks = max(1, -(-args.warmup // T))
-    n_chunks = max(1, -(-args.steps // T))
+    n_chunks = max(args.stats_every, -(-args.steps // T))
     steps = n_chunks * T
     for k in range(warm_chunks):
         chunk(k)
@@ -155,11 +207,15 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    G = max(1, args.event_group)
+    n_chunks = -(-n_chunks // G) * G
+    steps = n_chunks * T
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(n_chunks)]
+           for _ in range(n_chunks // G)]
     t0 = time.perf_counter()
     for k in range(n_chunks):
-        chunk(k, evs[k])
+        g = evs[k // G]
+        chunk(k, g if k % G == 0 else None, g[1] if k % G == G - 1 else None)
     if not args.no_stats:
         main.wait_stream(side)
         tot = stats.result()
@@ -168,8 +224,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sorted(a.elapsed_time(b) for a, b in evs)
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    kern_avg_ms = sum(a.elapsed_time(b) for a, b in evs) / (len(evs) * G)
     elapsed = pdist.max_over_ranks(elapsed, dev)
     kern_avg_ms = pdist.max_over_ranks(kern_avg_ms, dev)
 
@@ -203,12 +258,16 @@ def main():
                          "traffic": traffic,
                          "kernel": "k_rollout_wave (fenv_rollout)",
                          "algorithmic_bytes_per_launch": bytes_launch,
-                         "avg_kernel_ms": kern_avg_ms, "launches": n_chunks},
+                         "avg_kernel_ms": kern_avg_ms, "launches": n_chunks,
+                         "launches_per_event_pair": G},
         }
         if not args.no_stats:
             t = tot.cpu().tolist()
-            out["episode_stats"] = {"mean_reward": t[0] / (total_agents * T),
-                                    "agent_dones_last_rollout": t[1]}
+            out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * T),
+                                    "agent_dones_sampled_rollout": t[1],
+                                    "every_rollouts": args.stats_every}
+        if world == 1 and not args.no_policy:
+            out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)

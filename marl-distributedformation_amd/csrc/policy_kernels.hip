@@ -23,6 +23,10 @@
 
 namespace fenvk {
 
+#ifndef FENV_POLICY_V2
+#define FENV_POLICY_V2 0
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -60,22 +64,24 @@ constexpr int kHead = 3 * kHid + 3 + 2;       // Wa[2][64], Wv[64], ba[2], bv, l
 constexpr int kLds = kW1F + kW2F + kB + kHead;
 constexpr int oW1 = 0, oW2 = kW1F, oB1 = kW1F + kW2F, oB2 = oB1 + 2 * kHid, oHead = oB1 + kB;
 
-// Accurate single-precision tanh without libm calls: odd Taylor polynomial below 0.3,
-// 1 - 2/(1+e^{2|x|}) above (v_exp_f32 / v_rcp_f32); |rel err| < 5e-7 over all inputs.
+// Single-precision tanh without libm calls: odd/even minimax rational x P(x^2) / Q(x^2) on
+// [-7.9988, 7.9988] (clamped outside; Eigen's float tanh coefficients), one v_rcp_f32.
+// |abs err| < 4e-7 over all inputs (tests/test_gpu_policy.py bounds the network outputs).
 __device__ __forceinline__ float tanh_f(float x) {
-    const float ax = __builtin_fabsf(x);
-    const float x2 = x * x;
-    // tanh(x) = x + x^3 P(x^2), Taylor through x^13 (|x| < 0.3: truncation < 1e-10 relative)
-    float p = 21844.0f / 6081075.0f;
-    p = __builtin_fmaf(p, x2, -1382.0f / 155925.0f);
-    p = __builtin_fmaf(p, x2, 62.0f / 2835.0f);
-    p = __builtin_fmaf(p, x2, -17.0f / 315.0f);
-    p = __builtin_fmaf(p, x2, 2.0f / 15.0f);
-    p = __builtin_fmaf(p, x2, -1.0f / 3.0f);
-    const float ts = __builtin_fmaf(p, x2 * x, x);
-    const float e = __builtin_amdgcn_exp2f(ax * 2.88539008177792681f);  // e^{2|x|}
-    const float tl = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
-    return ax < 0.3f ? ts : __builtin_copysignf(tl, x);
+    const float xc = __builtin_amdgcn_fmed3f(x, -7.99881172180175781f, 7.99881172180175781f);
+    const float x2 = xc * xc;
+    float p = -2.76076847742355e-16f;
+    p = __builtin_fmaf(p, x2, 2.00018790482477e-13f);
+    p = __builtin_fmaf(p, x2, -8.60467152213735e-11f);
+    p = __builtin_fmaf(p, x2, 5.12229709037114e-08f);
+    p = __builtin_fmaf(p, x2, 1.48572235717979e-05f);
+    p = __builtin_fmaf(p, x2, 6.37261928875436e-04f);
+    p = __builtin_fmaf(p, x2, 4.89352455891786e-03f);
+    float q = 1.19825839466702e-06f;
+    q = __builtin_fmaf(q, x2, 1.18534705686654e-04f);
+    q = __builtin_fmaf(q, x2, 2.26843463243900e-03f);
+    q = __builtin_fmaf(q, x2, 4.89352518554385e-03f);
+    return (p * xc) * __builtin_amdgcn_rcpf(q);
 }
 
 __device__ __forceinline__ uint4 philox_p(uint4 c, uint32_t k0, uint32_t k1) {
@@ -152,6 +158,87 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
             const int col = 2 * s + h;
             o[s] = (valid && col < D) ? obs[row * D + col] : 0.0f;
         }
+#if FENV_POLICY_V2
+        float head[3] = {0.f, 0.f, 0.f};  // mu0, mu1 partials (actor), value partial (critic)
+        // Both networks in one straight-line body, ordered so that each MFMA phase has
+        // independent VALU work beside it: L1(pi,vf) | L2(pi) || tanh L1(vf) | L2(vf) || tanh
+        // L2(pi) + actor head | tanh L2(vf) + value head.
+        f32x16 pa0, pa1, va0, va1;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            pa0[reg] = lds[oB1 + rho(reg, h)];
+            pa1[reg] = lds[oB1 + 32 + rho(reg, h)];
+            va0[reg] = lds[oB1 + kHid + rho(reg, h)];
+            va1[reg] = lds[oB1 + kHid + 32 + rho(reg, h)];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (2 * s >= D) break;
+            pa0 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + (0 * 4 + s) * 64 + lane], o[s], pa0, 0, 0, 0);
+            pa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + (1 * 4 + s) * 64 + lane], o[s], pa1, 0, 0, 0);
+            va0 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + (2 * 4 + s) * 64 + lane], o[s], va0, 0, 0, 0);
+            va1 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + (3 * 4 + s) * 64 + lane], o[s], va1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            pa0[reg] = tanh_f(pa0[reg]);
+            pa1[reg] = tanh_f(pa1[reg]);
+        }
+        f32x16 pc0, pc1, vc0, vc1;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            pc0[reg] = lds[oB2 + rho(reg, h)];
+            pc1[reg] = lds[oB2 + 32 + rho(reg, h)];
+            vc0[reg] = lds[oB2 + kHid + rho(reg, h)];
+            vc1[reg] = lds[oB2 + kHid + 32 + rho(reg, h)];
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const f32x4 w0 = *reinterpret_cast<const f32x4 *>(&lds[oW2 + ((((0 * 2 + 0) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+                const f32x4 w1 = *reinterpret_cast<const f32x4 *>(&lds[oW2 + ((((0 * 2 + 1) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float b = kt == 0 ? pa0[4 * r4 + q] : pa1[4 * r4 + q];
+                    pc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[q], b, pc0, 0, 0, 0);
+                    pc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[q], b, pc1, 0, 0, 0);
+                    // independent VALU beside the actor's layer-2 MFMAs
+                    va0[4 * r4 + q + 0] = kt == 0 ? tanh_f(va0[4 * r4 + q]) : va0[4 * r4 + q];
+                    va1[4 * r4 + q + 0] = kt == 1 ? tanh_f(va1[4 * r4 + q]) : va1[4 * r4 + q];
+                }
+            }
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const f32x4 w0 = *reinterpret_cast<const f32x4 *>(&lds[oW2 + ((((1 * 2 + 0) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+                const f32x4 w1 = *reinterpret_cast<const f32x4 *>(&lds[oW2 + ((((1 * 2 + 1) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float b = kt == 0 ? va0[4 * r4 + q] : va1[4 * r4 + q];
+                    vc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[q], b, vc0, 0, 0, 0);
+                    vc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[q], b, vc1, 0, 0, 0);
+                    // actor head beside the critic's layer-2 MFMAs (same order as v1)
+                    const int reg = 4 * r4 + q;
+                    const f32x16 &pc = kt ? pc1 : pc0;
+                    const float hv = tanh_f(pc[reg]);
+                    const int idx = 32 * kt + rho(reg, h);
+                    head[0] = __builtin_fmaf(lds[oHead + idx], hv, head[0]);
+                    head[1] = __builtin_fmaf(lds[oHead + kHid + idx], hv, head[1]);
+                }
+            }
+        }
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const float hv = tanh_f(ot ? vc1[reg] : vc0[reg]);
+                head[2] = __builtin_fmaf(lds[oHead + 2 * kHid + 32 * ot + rho(reg, h)], hv, head[2]);
+            }
+        }
+#else
         float head[3] = {0.f, 0.f, 0.f};  // mu0, mu1 partials (actor), value partial (critic)
 #pragma unroll 1
         for (int net = 0; net < 2; ++net) {
@@ -224,6 +311,7 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
                 head[2] = pv;
             }
         }
+#endif
         // join the two lane halves in a fixed order (half 0 + half 1), add biases
         float full[3];
 #pragma unroll
@@ -270,10 +358,27 @@ hipError_t launch_policy_forward(const float *params, int32_t D, const float *ob
                                  float *mu, float *value, float *action, float *logp,
                                  float *clipped, uint64_t seed, uint64_t offset,
                                  int32_t deterministic, hipStream_t st) {
+    // Persistent grid sized to exactly the resident workgroups (no partial second round).
+    static int resident = 0;
+    if (resident == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_policy, 256, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus < 1)
+            cus = 256;
+        resident = per_cu * cus;
+    }
     const int64_t tiles = (B + 31) / 32;
     int64_t blocks = (tiles + 3) / 4;
-    const int64_t cap = 256 * 4;  // persistent: up to 4 workgroups (16 waves) per CU
-    if (blocks > cap) blocks = cap;
+    if (blocks > resident) {
+        // equalise tiles per wave over the resident grid
+        const int64_t rounds = (blocks + resident - 1) / resident;
+        blocks = (tiles + 4 * rounds - 1) / (4 * rounds);
+        if (blocks > resident) blocks = resident;
+    }
     hipLaunchKernelGGL(k_policy, dim3((unsigned)blocks), dim3(256), 0, st, params, D, obs, B, mu,
                        value, action, logp, clipped, seed, offset, deterministic);
     return hipGetLastError();

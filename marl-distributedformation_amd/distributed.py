@@ -29,10 +29,14 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob: run several ranks on fewer GPUs over gloo (never used by the driver)
+    backend = backend or os.environ.get("FENV_DIST_BACKEND") or None
+    if torch.cuda.is_available() and torch.cuda.device_count() > 0:
+        local = local % torch.cuda.device_count()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     return rank, world, local

@@ -96,28 +96,33 @@ class RolloutCollector:
         self.num_timesteps = 0
         self.last_obs = env.reset_tensor().clone()
         self.last_episode_starts = torch.ones(env.num_envs, dtype=torch.bool, device=env.device)
-        self._obs = torch.empty_like(self.last_obs)
-        self._rew = torch.empty(env.num_envs, dtype=torch.float32, device=env.device)
-        self._done = torch.empty(env.num_envs, dtype=torch.bool, device=env.device)
         self._last_values = torch.empty(env.num_envs, dtype=torch.float32, device=env.device)
 
     def collect(self, deterministic: bool = False) -> RolloutBuffer:
+        """n_steps x (policy_forward + fenv_step), two launches per step and no copies: the env
+        writes step k's observation straight into observations[k+1] and its dones into
+        episode_starts[k+1] (SB3's episode_starts are the previous step's dones)."""
         b = self.buffer
         b.reset()
-        for k in range(b.n_steps):
-            b.observations[k].copy_(self.last_obs)
-            self.policy.forward(self.last_obs, deterministic=deterministic,
+        T = b.n_steps
+        b.observations[0].copy_(self.last_obs)
+        b.episode_starts[0].copy_(self.last_episode_starts)
+        for k in range(T):
+            self.policy.forward(b.observations[k], deterministic=deterministic,
                                 out=dict(mu=b.mu[k], value=b.values[k], action=b.actions[k],
                                          log_prob=b.log_probs[k], clipped=b.clipped[k]),
                                 seed=self.seed, offset=self.offset)
             self.offset += 1
+            last = k == T - 1
             # the env is stepped with the clipped action (collect_rollouts np.clip)
-            self.env.step_tensor(b.clipped[k], obs=self._obs, rew=b.rewards[k], done=b.dones[k])
-            b.episode_starts[k].copy_(self.last_episode_starts)
-            self.last_obs.copy_(self._obs)
-            self.last_episode_starts.copy_(b.dones[k])
+            self.env.step_tensor(b.clipped[k],
+                                 obs=self.last_obs if last else b.observations[k + 1],
+                                 rew=b.rewards[k],
+                                 done=self.last_episode_starts if last else b.episode_starts[k + 1])
             self.num_timesteps += self.env.num_envs
             b.pos += 1
+        b.dones[:-1].copy_(b.episode_starts[1:])
+        b.dones[-1].copy_(self.last_episode_starts)
         self.policy.forward(self.last_obs, deterministic=True, out=dict(value=self._last_values),
                             seed=self.seed, offset=0)  # value of the final observation
         b.compute_returns_and_advantage(self._last_values, self.last_episode_starts)
