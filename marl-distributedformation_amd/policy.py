@@ -139,19 +139,3 @@ class MlpPolicy:
         r = self.forward(obs, deterministic=deterministic)
         return r["clipped"].cpu().numpy(), None
 
-
-def smoke_check(device="cuda:0") -> None:
-    """Small forward vs the torch-CPU restatement (oracle/policy_oracle.py)."""
-    import os
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                    "oracle"))
-    import policy_oracle as po
-    pol = MlpPolicy(8, device=device, seed=3)
-    g = torch.Generator().manual_seed(0)
-    obs = torch.rand((77, 8), generator=g) * 2 - 1
-    r = pol.forward(obs.to(device), deterministic=True)
-    mu, val = po.forward({k: v for k, v in pol.state_dict().items()}, obs)
-    torch.cuda.synchronize()
-    assert torch.allclose(r["mu"].cpu(), mu, rtol=1e-4, atol=1e-5), "policy mu mismatch"
-    assert torch.allclose(r["value"].cpu(), val, rtol=1e-4, atol=1e-5), "policy value mismatch"
