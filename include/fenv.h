@@ -146,6 +146,38 @@ int rollout_gae(const float *rew, const float *values, const uint8_t *episode_st
                 const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
                 float gamma, float gae_lambda, float *advantages, float *returns, void *stream);
 
+/* ------------------------------------------------------------------ fused PPO rollout
+ * Device buffers of one rollout (SB3 RolloutBuffer fields, vectorized_env.py:126-134 n_steps=T).
+ * Required: obs, action, value, log_prob, reward, episode_start, last_done.  Optional (NULL to
+ * skip): last_obs, mu, clipped, done, last_value, and advantage+ret (both or neither). */
+typedef struct fenv_rollout_bufs {
+    float *obs;             /* [T][A][D] observation each action was taken on */
+    float *last_obs;        /* [A][D] observation after the last step (SB3 _last_obs) */
+    float *mu;              /* [T][A][2] policy mean */
+    float *action;          /* [T][A][2] unclipped sampled action (what SB3 stores) */
+    float *clipped;         /* [T][A][2] clamp(action, -1, 1): what the env was stepped with */
+    float *value;           /* [T][A] critic value of obs */
+    float *log_prob;        /* [T][A] */
+    float *reward;          /* [T][A] */
+    uint8_t *episode_start; /* [T][A] 1 where the step began an episode (previous step's done) */
+    uint8_t *done;          /* [T][A] */
+    uint8_t *last_done;     /* [A] in: episode_start of step 0; out: done of the last step */
+    float *last_value;      /* [A] value of last_obs */
+    float *advantage;       /* [T][A] GAE(lambda) advantages */
+    float *ret;             /* [T][A] advantage + value */
+} fenv_rollout_bufs;
+
+/* SB3 collect_rollouts + compute_returns_and_advantage: T steps of every agent in ONE kernel
+ * launch -- per step the policy forward (as policy_forward with seed and counter offset+k) and
+ * the env step with the clipped action (as fenv_step), then the value of the final observation
+ * -- followed by one GAE launch (as rollout_gae) when advantage/ret are given.  Observation 0 is the env's
+ * current observation.  Results are bit-identical to the unfused calls.  Formation sizes
+ * 1 <= N <= 64 (larger formations: policy_forward + fenv_step).  In FENV_RESET_MT19937 mode a
+ * launch may contain at most one reset event (T <= max_steps + 2). */
+int fenv_policy_rollout(fenv_t *env, const float *params, int32_t T, uint64_t seed,
+                        uint64_t offset, int32_t deterministic, float gamma, float gae_lambda,
+                        const fenv_rollout_bufs *bufs, void *stream);
+
 const char *fenv_last_error(void);
 
 #ifdef __cplusplus

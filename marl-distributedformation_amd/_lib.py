@@ -50,8 +50,17 @@ SIGNATURES = {
     "policy_forward": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _U64, _U64, _I32, _P]),
     "rollout_gae": (_I32, [_P, _P, _P, _P, _P, _I32, _I64, ctypes.c_float, ctypes.c_float, _P, _P,
                            _P]),
+    "fenv_policy_rollout": (_I32, [_P, _P, _I32, _U64, _U64, _I32, ctypes.c_float,
+                                   ctypes.c_float, _P, _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
+
+
+class RolloutBufs(ctypes.Structure):
+    """``fenv_rollout_bufs`` (include/fenv.h): device pointers of one fused rollout."""
+    _fields_ = [(n, _P) for n in ("obs", "last_obs", "mu", "action", "clipped", "value",
+                                  "log_prob", "reward", "episode_start", "done", "last_done",
+                                  "last_value", "advantage", "ret")]
 
 
 class FenvError(RuntimeError):

@@ -66,6 +66,7 @@ struct fenv {
     float *hpend = nullptr;  // pinned host staging for `pend`
     hipEvent_t pend_ev = nullptr;
     bool pend_ev_recorded = false;
+    float *lv_scratch = nullptr;  // last values for GAE when the caller passes none
     std::mt19937 mt;         // the reference's global stream (all formations of all shards)
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
 
@@ -203,6 +204,7 @@ int fenv_destroy(fenv_t *e) {
     if (e->pend) (void)hipFree(e->pend);
     if (e->hpend) (void)hipHostFree(e->hpend);
     if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
+    if (e->lv_scratch) (void)hipFree(e->lv_scratch);
     delete e;
     return FENV_OK;
 }
@@ -367,6 +369,64 @@ int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64
     if (B == 0) return FENV_OK;
     FENV_HIP(fenvk::launch_policy_forward(params, obs_dim, obs, B, mu, value, action, logp, clipped,
                                          seed, offset, deterministic, as_stream(stream)));
+    return FENV_OK;
+}
+
+int fenv_policy_rollout(fenv_t *e, const float *params, int32_t T, uint64_t seed,
+                        uint64_t offset, int32_t deterministic, float gamma, float gae_lambda,
+                        const fenv_rollout_bufs *bufs, void *stream) {
+    if (!e || !params || !bufs) return fail(FENV_EINVAL, "fenv_policy_rollout: NULL argument");
+    if (T < 1) return fail(FENV_EINVAL, "fenv_policy_rollout: T must be >= 1");
+    const fenv_rollout_bufs &b = *bufs;
+    if (!b.obs || !b.action || !b.value || !b.log_prob || !b.reward || !b.episode_start ||
+        !b.last_done)
+        return fail(FENV_EINVAL, "fenv_policy_rollout: obs, action, value, log_prob, reward, "
+                                 "episode_start and last_done are required");
+    if ((b.advantage == nullptr) != (b.ret == nullptr))
+        return fail(FENV_EINVAL, "fenv_policy_rollout: advantage and ret go together");
+    if (!fenvk::wave_path(e->c.N))
+        return fail(FENV_EINVAL, "fenv_policy_rollout: num_agents must be <= 64 "
+                                 "(use policy_forward + fenv_step for larger formations)");
+    FENV_HIP(hipSetDevice(e->device));
+    hipStream_t st = as_stream(stream);
+    bool event = false;
+    if (e->c.reset_mode == FENV_RESET_MT19937) {
+        if (e->t_common < 0)
+            return fail(FENV_ESTATE, "MT19937 reset mode needs formations in lock-step");
+        const int64_t je = std::max<int64_t>(0, (int64_t)e->c.max_steps + 1 - e->t_common);
+        if (je < T) {
+            event = true;
+            if (je + (int64_t)e->c.max_steps + 2 < T)
+                return fail(FENV_EINVAL, "fenv_policy_rollout: more than one reset event in one "
+                                         "launch (T > max_steps + 2) in MT19937 mode");
+        }
+    }
+    const bool gae = b.advantage != nullptr;
+    fenvk::PRArgs g{};
+    g.b = b;
+    g.params = params;
+    g.T = T;
+    g.deterministic = deterministic;
+    g.seed = seed;
+    g.offset = offset;
+    g.gamma = gamma;
+    g.lam = gae_lambda;
+    if (gae && !b.last_value) {  // GAE needs the last values
+        if (!e->lv_scratch) {
+            hipError_t he = hipMalloc(&e->lv_scratch, (size_t)e->A * sizeof(float));
+            if (he != hipSuccess) return fail(FENV_ENOMEM, "hipMalloc(last_value scratch) failed");
+        }
+        g.b.last_value = e->lv_scratch;
+    }
+    FENV_HIP(fenvk::launch_policy_rollout(e->c, e->s, e->pending(), e->D, g, st));
+    e->advance_t(T);
+    if (event) {
+        int rc = e->gen_pending(st);
+        if (rc) return rc;
+    }
+    if (gae)
+        FENV_HIP(fenvk::launch_gae(b.reward, b.value, b.episode_start, g.b.last_value, b.last_done,
+                                   T, e->A, gamma, gae_lambda, b.advantage, b.ret, st));
     return FENV_OK;
 }
 

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include "fenv.h"
+
 namespace fenvk {
 
 // Device-resident env state, structure-of-arrays (one lane reads 8 B of position per agent,
@@ -54,6 +56,18 @@ hipError_t launch_policy_forward(const float *params, int32_t D, const float *ob
                                  float *mu, float *value, float *action, float *logp,
                                  float *clipped, uint64_t seed, uint64_t offset,
                                  int32_t deterministic, hipStream_t st);
+
+// Fused policy->env rollout (policy_rollout.hip); GAE follows as a launch_gae.
+struct PRArgs {
+    fenv_rollout_bufs b;
+    const float *params;
+    int32_t T;
+    int32_t deterministic;
+    uint64_t seed, offset;
+    float gamma, lam;
+};
+hipError_t launch_policy_rollout(const Consts &c, const DevState &s, const DevPending &p,
+                                 int32_t D, const PRArgs &g, hipStream_t st);
 
 hipError_t launch_gae(const float *rew, const float *values, const uint8_t *episode_starts,
                       const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,

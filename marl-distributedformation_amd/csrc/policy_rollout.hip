@@ -1,0 +1,226 @@
+// Fused PPO rollout collection on gfx950: per step, the policy forward on the MFMA cores ->
+// Gaussian sample -> clip -> formation-env step -> next observation, T steps in one launch,
+// then the value of the final observation.
+//
+// Reference: SB3 OnPolicyAlgorithm.collect_rollouts + RolloutBuffer as driven by
+// PPO('MlpPolicy', env, n_steps=10, ...) (/root/reference/vectorized_env.py:126-134) over
+// FormationEnv.step (vectorized_env.py:68-82) -> FormationSimulator.step (simulate.py:70-118).
+// Bit-identical to the unfused path (policy_forward + fenv_step per step, then rollout_gae):
+// the policy math is policy_device.h, the env math env_device.h, GAE gae_step.
+//
+// Mapping.  A wavefront owns fpw = 64/N whole formations (M = fpw*N <= 64 agents, lane = agent)
+// for all T steps, exactly as k_rollout_wave; its agents are two 32-agent MFMA tiles.  Per step
+// the observation rows are staged in the wave's private 2 KiB LDS slice (coalesced store to
+// observations[k] and the MFMA B operands come from the same slice), the policy outputs are
+// staged in the same slice (coalesced stores of mu/action/clipped/value/log_prob, and the lane
+// that owns agent l picks up its clipped action), then the env step runs on registers.
+// 8 waves per workgroup share one 38.7 KB weight image; <= 128 VGPRs keeps 4 waves per SIMD.
+// GAE runs as one short HBM-bound launch after it (k_gae: 17 B per agent-step, ~2 % of the
+// rollout; holding T rewards and values in registers would cost the occupancy).
+//
+// Roofline: MFMA fp32 (18,816 FLOP per agent-step + 9,344 per agent for the last value);
+// HBM output is ~78 B per agent-step, an order of magnitude below the MFMA time.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "env_device.h"
+#include "policy_device.h"
+
+namespace fenvk {
+
+constexpr int kPRWaves = 8;
+// 4 waves per SIMD (<= 128 VGPRs): what the 55 KB of LDS per 8-wave workgroup allows anyway
+#ifndef FENV_PR_OCCUPANCY
+#define FENV_PR_OCCUPANCY __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+constexpr size_t kPRLdsBytes = (size_t)(kPolicyLds + kPRWaves * 512) * sizeof(float);
+static_assert(kPolicyLds % 4 == 0, "stage slices must stay 16-byte aligned");
+
+// Copy nf floats from a wave's LDS slice to global memory with the widest aligned stores.
+__device__ __forceinline__ void store_span(const float *stage, int nf, float *dst, int lane) {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if ((ad & 15) == 0 && (nf & 3) == 0) {
+        for (int q = lane; q < (nf >> 2); q += 64)
+            reinterpret_cast<float4 *>(dst)[q] = reinterpret_cast<const float4 *>(stage)[q];
+    } else if ((ad & 7) == 0 && (nf & 1) == 0) {
+        for (int q = lane; q < (nf >> 1); q += 64)
+            reinterpret_cast<float2 *>(dst)[q] = reinterpret_cast<const float2 *>(stage)[q];
+    } else {
+        for (int q = lane; q < nf; q += 64) dst[q] = stage[q];
+    }
+}
+
+// The MFMA B operands of the wave's two tiles from the staged observation rows.
+template <int D>
+__device__ __forceinline__ void tile_operands(const float *stage, int j, int h, float (&ob)[2][4]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int col = 2 * s + h;
+            ob[t][s] = col < D ? stage[(32 * t + j) * D + col] : 0.0f;
+        }
+}
+
+template <int D, int MODE>
+__global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_rollout(Consts c, DevState st,
+                                                                  DevPending p, PRArgs g) {
+    // Dynamic LDS (kPRLdsBytes, set at launch): with a static 55 KB declaration the compiler
+    // budgets registers for 2 waves/SIMD and schedules into 220+ VGPRs; sized at launch it keeps
+    // the 4 waves/SIMD that the LDS actually allows (2 workgroups per CU).
+    extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+    float *wimg = lds_dyn;
+    float(*stage_all)[512] = reinterpret_cast<float(*)[512]>(lds_dyn + kPolicyLds);
+    stage_policy_weights(wimg, g.params, D, threadIdx.x, blockDim.x);
+    __syncthreads();  // the only workgroup barrier: waves are independent from here on
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR
+    const int64_t wave = (int64_t)blockIdx.x * kPRWaves + w;
+    const int64_t f_first = wave * c.fpw;
+    if (f_first >= c.F) return;
+    const int N = c.N;
+    const int fi = lane / N;
+    const int i = lane - fi * N;
+    const int64_t f = f_first + fi;
+    const bool active = fi < c.fpw && f < c.F;
+    const int64_t a = f * N + i;
+    const WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
+    const int64_t f_left = c.F - f_first;
+    const int M = (int)((f_left < c.fpw ? f_left : c.fpw) * N);
+    const int64_t a_first = f_first * N;
+    const int64_t A = c.F * (int64_t)N;
+    float *stage = stage_all[w];
+    const fenv_rollout_bufs &b = g.b;
+    const bool det = g.deterministic != 0;
+
+    Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
+    uint32_t start = 0;  // episode_start of the current step (SB3: previous step's done)
+    if (active) {
+        s.px = st.px[a];
+        s.py = st.py[a];
+        s.gx = st.gx[f];
+        s.gy = st.gy[f];
+        s.t = st.t[f];
+        s.ep = st.ep[f];
+        start = b.last_done[a] ? 1u : 0u;
+    }
+    bool any_reset = false;
+
+    float o[8];
+    env_obs<D>(x, s, o);
+    for (int32_t k = 0; k < g.T; ++k) {
+        // weights are re-read from LDS every step: keeps the compiler from hoisting the
+        // loop-invariant LDS image into (spilled) registers
+        asm volatile("" ::: "memory");
+        // an opaque copy of the lane index: every LDS address derived from it is recomputed per
+        // step instead of being hoisted into ~85 loop-invariant VGPRs
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int j = ln & 31, h = ln >> 5;
+        const int64_t rk = (int64_t)k * A;
+        // the observation the action is taken on -> observations[k]
+        store_obs_rows<D>(stage, o, ln, M, b.obs + (rk + a_first) * D);
+        float ob[2][4];
+        tile_operands<D>(stage, j, h, ob);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            // one tile at a time, outputs parked in LDS at once (keeps the step under 128 VGPRs)
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            const PolicyLane pl = policy_tile(wimg, ob[t], D, ln, a_first + 32 * t + j, g.seed,
+                                              g.offset + k, det, false);
+            const int r = 32 * t + j;
+            stage[2 * r + h] = pl.mu;
+            stage[128 + 2 * r + h] = pl.act;
+            stage[256 + 2 * r + h] = pl.clip;
+            if (h == 0) {
+                stage[384 + r] = pl.value;
+                stage[448 + r] = pl.logp;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (b.mu) store_span(stage, 2 * M, b.mu + (rk + a_first) * 2, ln);
+        store_span(stage + 128, 2 * M, b.action + (rk + a_first) * 2, ln);
+        if (b.clipped) store_span(stage + 256, 2 * M, b.clipped + (rk + a_first) * 2, ln);
+        store_span(stage + 384, M, b.value + rk + a_first, ln);
+        store_span(stage + 448, M, b.log_prob + rk + a_first, ln);
+        const float2 ac = reinterpret_cast<const float2 *>(stage + 256)[ln];
+        __builtin_amdgcn_wave_barrier();
+
+        // env.step(clipped actions) (collect_rollouts clips to the Box, vectorized_env.py:68-82)
+        float rw;
+        bool dn, rs;
+        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        any_reset |= rs;
+        if (active) {
+            b.reward[rk + a] = rw;
+            b.episode_start[rk + a] = (uint8_t)start;
+            if (b.done) b.done[rk + a] = (uint8_t)dn;
+        }
+        start = dn ? 1u : 0u;
+        env_obs<D>(x, s, o);
+    }
+
+    // the observation after the last step (SB3's self._last_obs) and its value
+    if (b.last_obs) {
+        store_obs_rows<D>(stage, o, lane, M, b.last_obs + a_first * D);
+    } else {
+        stage_obs_rows<D>(stage, o, lane);
+        __builtin_amdgcn_wave_barrier();
+    }
+    float lv = 0.0f;
+    if (b.last_value) {
+        const int j = lane & 31, h = lane >> 5;
+        float ob[2][4];
+        tile_operands<D>(stage, j, h, ob);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            const PolicyLane pv = policy_tile(wimg, ob[t], D, lane, 0, 0, 0, true, true);
+            if (h == 0) stage[384 + 32 * t + j] = pv.value;
+        }
+        __builtin_amdgcn_wave_barrier();
+        lv = stage[384 + lane];
+    }
+    if (active) {
+        b.last_done[a] = (uint8_t)start;
+        if (b.last_value) b.last_value[a] = lv;
+        st.px[a] = s.px;
+        st.py[a] = s.py;
+        if (i == 0) {
+            st.t[f] = s.t;
+            if (any_reset) {
+                st.gx[f] = s.gx;
+                st.gy[f] = s.gy;
+                st.ep[f] = s.ep;
+            }
+        }
+    }
+}
+
+template <int D, int MODE>
+static hipError_t policy_rollout_dm(const Consts &c, const DevState &s, const DevPending &p,
+                                    const PRArgs &g, hipStream_t st) {
+    const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
+    const unsigned blocks = (unsigned)((waves + kPRWaves - 1) / kPRWaves);
+    hipLaunchKernelGGL((k_policy_rollout<D, MODE>), dim3(blocks), dim3(64 * kPRWaves), kPRLdsBytes,
+                       st, c, s, p, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_policy_rollout(const Consts &c, const DevState &s, const DevPending &p,
+                                 int32_t D, const PRArgs &g, hipStream_t st) {
+    const bool mt = c.reset_mode == FENV_RESET_MT19937;
+    if (D == 8)
+        return mt ? policy_rollout_dm<8, FENV_RESET_MT19937>(c, s, p, g, st)
+                  : policy_rollout_dm<8, FENV_RESET_PHILOX>(c, s, p, g, st);
+    return mt ? policy_rollout_dm<6, FENV_RESET_MT19937>(c, s, p, g, st)
+              : policy_rollout_dm<6, FENV_RESET_PHILOX>(c, s, p, g, st);
+}
+
+}  // namespace fenvk

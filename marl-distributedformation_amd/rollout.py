@@ -85,20 +85,51 @@ class RolloutBuffer:
 
 
 class RolloutCollector:
-    """SB3 ``collect_rollouts`` on device: policy forward + env step per step, no host copies."""
+    """SB3 ``collect_rollouts`` on device.
 
-    def __init__(self, env, policy, buffer: RolloutBuffer, seed: int = 0):
+    ``fused=True`` (default whenever the formation fits a wavefront, N <= 64) runs the whole
+    rollout -- T x (policy forward + env step), last value, GAE -- as ONE kernel
+    (``fenv_policy_rollout``); ``fused=False`` issues policy_forward + fenv_step per step and a
+    GAE launch.  Both produce identical bits (tests/test_gpu_rollout.py)."""
+
+    def __init__(self, env, policy, buffer: RolloutBuffer, seed: int = 0,
+                 fused: bool | None = None):
         if buffer.n_envs != env.num_envs or buffer.obs_dim != env.obs_dim:
             raise ValueError("buffer shape does not match the env")
         self.env, self.policy, self.buffer = env, policy, buffer
+        self.fused = env.num_agents_per_formation <= 64 if fused is None else bool(fused)
         self.seed = int(seed)
         self.offset = 0
         self.num_timesteps = 0
         self.last_obs = env.reset_tensor().clone()
         self.last_episode_starts = torch.ones(env.num_envs, dtype=torch.bool, device=env.device)
+        # torch.bool is one byte per element: the kernels read/write it as uint8
         self._last_values = torch.empty(env.num_envs, dtype=torch.float32, device=env.device)
 
     def collect(self, deterministic: bool = False) -> RolloutBuffer:
+        if self.fused:
+            return self._collect_fused(deterministic)
+        return self._collect_steps(deterministic)
+
+    def _collect_fused(self, deterministic: bool) -> RolloutBuffer:
+        b = self.buffer
+        b.reset()
+        T = b.n_steps
+        self.env.policy_rollout(
+            self.policy.flat, T, dict(
+                obs=b.observations, last_obs=self.last_obs, mu=b.mu, action=b.actions,
+                clipped=b.clipped, value=b.values, log_prob=b.log_probs, reward=b.rewards,
+                episode_start=b.episode_starts, done=b.dones,
+                last_done=self.last_episode_starts, last_value=self._last_values,
+                advantage=b.advantages, ret=b.returns),
+            seed=self.seed, offset=self.offset, deterministic=deterministic, gamma=b.gamma,
+            gae_lambda=b.gae_lambda)
+        self.offset += T
+        self.num_timesteps += T * self.env.num_envs
+        b.pos = T
+        return b
+
+    def _collect_steps(self, deterministic: bool) -> RolloutBuffer:
         """n_steps x (policy_forward + fenv_step), two launches per step and no copies: the env
         writes step k's observation straight into observations[k+1] and its dones into
         episode_starts[k+1] (SB3's episode_starts are the previous step's dones)."""

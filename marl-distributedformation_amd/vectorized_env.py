@@ -313,6 +313,28 @@ class FormationEnv:
                                            self._stream()), "fenv_rollout")
         return obs, rew, done
 
+    def policy_rollout(self, params: torch.Tensor, T: int, bufs: dict, seed: int = 0,
+                       offset: int = 0, deterministic: bool = False, gamma: float = 0.99,
+                       gae_lambda: float = 0.95) -> None:
+        """One fused launch (``fenv_policy_rollout``): T steps of policy forward (SB3 MlpPolicy
+        on the flat ``params``) + env step, then the last value and GAE, written into the
+        device tensors of ``bufs`` (keys = the fields of ``fenv_rollout_bufs``: obs, last_obs,
+        mu, action, clipped, value, log_prob, reward, episode_start, done, last_done,
+        last_value, advantage, ret; missing optional keys are skipped)."""
+        if params.dtype != torch.float32 or params.device != self.device:
+            raise TypeError(f"params must be float32 on {self.device}")
+        rb = _lib.RolloutBufs()
+        for name, _ in _lib.RolloutBufs._fields_:
+            t = bufs.get(name)
+            if t is not None:
+                if t.device != self.device or not t.is_contiguous():
+                    raise ValueError(f"{name}: must be a contiguous tensor on {self.device}")
+                setattr(rb, name, t.data_ptr())
+        _lib.check(_lib.lib().fenv_policy_rollout(
+            self._h, _lib.ptr(params), int(T), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset),
+            int(bool(deterministic)), float(gamma), float(gae_lambda), ctypes.byref(rb),
+            self._stream()), "fenv_policy_rollout")
+
     def partial_count(self) -> int:
         return int(_lib.lib().fenv_partial_count(self._h))
 

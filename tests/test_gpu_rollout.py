@@ -102,3 +102,65 @@ def test_ppo_learns(mods):
     assert all(np.isfinite(v) for v in ppo.stats.values())
     # learning signal: the average reward of the last rollouts beats the first ones
     assert np.mean(rewards[-5:]) > np.mean(rewards[:5])
+
+
+FIELDS = ("observations", "actions", "clipped", "mu", "values", "log_probs", "rewards",
+          "episode_starts", "dones", "advantages", "returns")
+
+
+@pytest.mark.parametrize("F,N,goal,T,mode,max_steps,det", [
+    (300, 5, True, 10, "mt19937", 13, False),    # reset events inside rollouts, 12 fm / wave
+    (1001, 10, True, 10, "philox", 23, False),   # BASELINE config-2 shape (scaled), tail wave
+    (37, 64, True, 6, "mt19937", 9, False),      # one formation per wavefront
+    (50, 7, False, 8, "philox", 11, True),       # D = 6, 9 formations / wave, deterministic
+    (40, 5, True, 20, "philox", 7, False),       # T > 16: GAE as a separate launch
+    (9, 33, True, 3, "mt19937", 1000, False),    # M = 33: second tile has one agent
+])
+def test_fused_rollout_matches_unfused(mods, F, N, goal, T, mode, max_steps, det):
+    """fenv_policy_rollout (one kernel per rollout) == policy_forward + fenv_step per step +
+    rollout_gae, bit for bit, over several consecutive rollouts (episode boundaries inside)."""
+    D = 8 if goal else 6
+    cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": goal}
+    ve, ro = mods["vectorized_env"], mods["rollout"]
+    envs = [ve.FormationEnv(cfg, device=DEV, seed=4, reset_mode=mode, max_steps=max_steps)
+            for _ in range(2)]
+    pol = mods["policy"].MlpPolicy(D, device=DEV, seed=1)
+    g = torch.Generator().manual_seed(N)
+    with torch.no_grad():  # non-trivial heads so actions move the agents
+        pol.flat.add_(torch.randn(pol.flat.shape, generator=g).to(DEV) * 0.05)
+    bufs = [ro.RolloutBuffer(T, F * N, D, DEV) for _ in range(2)]
+    cols = [ro.RolloutCollector(envs[0], pol, bufs[0], seed=7, fused=True),
+            ro.RolloutCollector(envs[1], pol, bufs[1], seed=7, fused=False)]
+    saw_done = False
+    for r in range(4):
+        for c in cols:
+            c.collect(deterministic=det)
+        torch.cuda.synchronize()
+        for name in FIELDS:
+            a, b = getattr(bufs[0], name), getattr(bufs[1], name)
+            assert torch.equal(a, b), f"rollout {r}: {name} differs"
+        saw_done |= bool(bufs[0].dones.any())
+        assert torch.equal(cols[0].last_obs, cols[1].last_obs)
+        assert torch.equal(cols[0].last_episode_starts, cols[1].last_episode_starts)
+        assert torch.equal(cols[0]._last_values, cols[1]._last_values)
+        for sa, sb in zip(envs[0].get_state(), envs[1].get_state()):
+            assert torch.equal(sa, sb), f"rollout {r}: env state differs"
+    assert cols[0].num_timesteps == cols[1].num_timesteps == 4 * T * F * N
+    if max_steps + 2 <= 4 * T:
+        assert saw_done
+
+
+def test_fused_rollout_errors(mods, flib):
+    ve, ro = mods["vectorized_env"], mods["rollout"]
+    env = ve.FormationEnv({"num_formation": 3, "num_agents_per_formation": 65,
+                           "goal_in_obs": True}, device=DEV, seed=0)
+    pol = mods["policy"].MlpPolicy(8, device=DEV)
+    col = ro.RolloutCollector(env, pol, ro.RolloutBuffer(4, 195, 8, DEV), seed=0)
+    assert not col.fused  # N > 64 falls back to the per-step HIP path
+    col.collect()
+    with pytest.raises(flib.FenvError, match="num_agents must be <= 64"):
+        ro.RolloutCollector(env, pol, ro.RolloutBuffer(4, 195, 8, DEV), fused=True).collect()
+    env2 = ve.FormationEnv({"num_formation": 3, "num_agents_per_formation": 5,
+                            "goal_in_obs": True}, device=DEV, seed=0, max_steps=3)
+    with pytest.raises(flib.FenvError, match="more than one reset event"):
+        ro.RolloutCollector(env2, pol, ro.RolloutBuffer(12, 15, 8, DEV), fused=True).collect()
