@@ -32,6 +32,10 @@ namespace fenvk {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef FENV_POLICY_PRIO
+#define FENV_POLICY_PRIO 0
+#endif
+
 constexpr int kHid = 64;
 constexpr float kTanhScale = 2.88539008177792681f;  // 2 / ln(2)
 
@@ -148,6 +152,9 @@ __device__ __forceinline__ void net_tile(const float *lds, int net, const float 
     }
     c0 = bias_acc(lds + oB2 + net * kHid, 0, h);
     c1 = bias_acc(lds + oB2 + net * kHid, 1, h);
+#if FENV_POLICY_PRIO
+    __builtin_amdgcn_s_setprio(1);  // a wave in its MFMA phase wins issue arbitration
+#endif
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
@@ -164,6 +171,9 @@ __device__ __forceinline__ void net_tile(const float *lds, int net, const float 
             }
         }
     }
+#if FENV_POLICY_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         c0[reg] = tanh_s(c0[reg]);

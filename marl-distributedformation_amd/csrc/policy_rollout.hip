@@ -14,7 +14,11 @@
 // observations[k] and the MFMA B operands come from the same slice), the policy outputs are
 // staged in the same slice (coalesced stores of mu/action/clipped/value/log_prob, and the lane
 // that owns agent l picks up its clipped action), then the env step runs on registers.
-// 8 waves per workgroup share one 38.7 KB weight image; <= 128 VGPRs keeps 4 waves per SIMD.
+// 4 waves per workgroup share one 38.7 KB weight image (46.7 KB of LDS with the stage slices:
+// 3 workgroups per CU); <= 128 VGPRs.  A wave in its MFMA phase raises its issue priority
+// (s_setprio) so the VALU/LDS work of the other waves fills around it.  Measured against 8-wave
+// workgroups with and without the priority (build_variants, tools/gpu_policy.sh): 4 waves +
+// priority is +9 % at F = 65,536 x 10 and +2 % at F = 262,144 x 10.
 // GAE runs as one short HBM-bound launch after it (k_gae: 17 B per agent-step, ~2 % of the
 // rollout; holding T rewards and values in registers would cost the occupancy).
 //
@@ -24,13 +28,19 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef FENV_POLICY_PRIO
+#define FENV_POLICY_PRIO 1
+#endif
 #include "env_device.h"
 #include "policy_device.h"
 
 namespace fenvk {
 
-constexpr int kPRWaves = 8;
-// 4 waves per SIMD (<= 128 VGPRs): what the 55 KB of LDS per 8-wave workgroup allows anyway
+#ifndef FENV_PR_WAVES
+#define FENV_PR_WAVES 4
+#endif
+constexpr int kPRWaves = FENV_PR_WAVES;
+// <= 128 VGPRs per wave
 #ifndef FENV_PR_OCCUPANCY
 #define FENV_PR_OCCUPANCY __attribute__((amdgpu_waves_per_eu(4)))
 #endif
