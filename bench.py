@@ -97,13 +97,18 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
         b.record()
     torch.cuda.synchronize()
     pk_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    flop = 18816.0 * A
+    flop = 18816.0 * A           # fp32-equivalent FLOP of one policy_forward over the batch
+    f16 = 57344.0 * A            # split-f16 MFMA FLOP actually issued (56 MFMAs per 32 agents)
     return {"workload": f"config2: {formations} formations x {agents} agents, PPO rollout "
-                        f"(n_steps=10): MFMA policy forward + env step per step, GAE",
+                        f"(n_steps=10): fused MFMA policy forward + env step per step, GAE",
             "value": A * 10 * rollouts / el, "unit": "agent-steps/s",
-            "policy_kernel_ms": pk_ms, "policy_tflops": flop / (pk_ms * 1e-3) / 1e12,
-            "mfma_fp32_peak_tflops": 157.3,
-            "mfma_frac": flop / (pk_ms * 1e-3) / 1e12 / 157.3}
+            "policy_kernel_ms": pk_ms,
+            "policy_fp32_equiv_tflops": flop / (pk_ms * 1e-3) / 1e12,
+            "policy_f16_mfma_tflops": f16 / (pk_ms * 1e-3) / 1e12,
+            "f16_mfma_dense_peak_tflops": 2516.6,
+            "f16_mfma_frac": f16 / (pk_ms * 1e-3) / 1e12 / 2516.6,
+            "arithmetic": "split-f16 MFMA (hi*hi + hi*lo + lo*hi, fp32 accumulate), fp32 tanh/heads",
+            "bound": "VALU issue (256 exp+rcp tanh per agent-step), see DESIGN.md"}
 
 
 def load_pmc_traffic(workload: str):

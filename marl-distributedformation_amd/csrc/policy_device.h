@@ -8,19 +8,33 @@
 // a = mu + exp(log_std) * eps, stores log_prob, and hands clip(a, -1, 1) to env.step;
 // predict(deterministic=True) (/root/reference/visualize_policy.py:16) returns clip(mu).
 //
-// Mapping (one wavefront = one 32-agent tile):
-//   layer 1  H1^T[64 x 32] = W1[64 x D] . O^T[D x 32]     v_mfma_f32_32x32x2_f32, 2 row tiles x D/2
-//   layer 2  H2^T[64 x 32] = W2[64 x 64] . tanh(H1^T)     the layer-1 accumulator registers ARE the
-//            B operands (lane l holds hidden rows rho(r, l>>5) of agent l&31), so no data moves
-//            between layers; W2 is read from LDS pre-permuted into that k order (ds_read_b128).
-//   heads    mu[2], value on the VALU from the layer-2 accumulators, halves joined across lanes
-//            l and l^32.
-// Both networks: 144 MFMAs of 32x32x2 per 32 agents = 18,816 FLOP/agent.
+// Arithmetic: split-f16 MFMA ("3xf16").  Every fp32 operand x is split as x = hi + lo with
+// hi = x truncated to 11 significant bits and lo = the exact remainder rounded to f16, and each
+// fp32 product is taken as hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16 (products exact,
+// fp32 accumulation; the dropped lo*lo term and lo's rounding are < 2^-21 relative).  Three
+// 32-cycle f16 MFMAs replace eight 64-cycle f32 32x32x2 MFMAs per 16-deep k-chunk: the policy
+// tile's MFMA time drops ~5x while the results stay within the fp32 tolerance
+// (tests/test_gpu_policy.py; numpy emulation tools/split_f16_error.py: worst error 17 % of the
+// 2e-5 + 2e-5|ref| bound).  Operand-map, subnormal and exactness facts this relies on are probed
+// on the hardware by tools/mfma_f16_probe.hip.  Inputs must satisfy |x| < 65504 (f16 range);
+// the env's observations are within [-1.5, 1.5].
+//
+// Mapping (one wavefront = one 32-agent tile, lane l: agent r = l&31, half h = l>>5):
+//   layer 1  H1^T[64 x 32] = W1[64 x D] . O^T[D x 32]: per 32-row tile two MFMAs over a 16-slot
+//            k: slots 0-7 (half 0) carry (W1hi, Ohi), slots 8-15 (half 1) (W1hi, Olo); then
+//            (W1lo, Ohi) in half 0 and zeros in half 1.
+//   layer 2  H2^T[64 x 32] = W2[64 x 64] . tanh(H1^T): the layer-1 accumulator registers ARE the
+//            B operands (chunk c = registers 8(c&1)..+7 of row tile c>>1, i.e. hidden rows
+//            32(c>>1) + rho(8(c&1)+j, h)); W2 is staged in LDS pre-permuted into that k order as
+//            hi and lo fragments (one ds_read_b128 each).  4 chunks x 3 products per row tile.
+//   heads    mu[2], value on the VALU (fp32 FMA) from the layer-2 accumulators, halves joined
+//            across lanes l and l^32.
+// Both networks: 56 f16 MFMAs per 32 agents carrying 18,816 fp32-equivalent FLOP/agent
+// (SURVEY §8(a) R10).
 //
 // tanh.  Hidden-layer weights and biases are staged pre-multiplied by 2/ln2, so an accumulator
-// holds y = 2x*log2(e) and tanh(x) = 1 - 2 / (1 + 2^y): v_exp_f32, v_add, v_rcp_f32, v_fma --
-// 4 VALU instructions instead of a 13-instruction rational, which is what lets the VALU work hide
-// under the MFMAs.  |abs err| < 5e-7 (tests/test_gpu_policy.py bounds the network outputs).
+// holds y = 2x*log2(e) and tanh(x) = 1 - 2 / (1 + 2^y): v_exp_f32, v_add, v_rcp_f32, v_fma.
+// |abs err| < 5e-7.
 #pragma once
 #pragma clang fp contract(off)
 
@@ -31,6 +45,8 @@ namespace fenvk {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef FENV_POLICY_PRIO
 #define FENV_POLICY_PRIO 0
@@ -63,35 +79,74 @@ struct PLayout {
     }
 };
 
-// LDS image (floats).  net 0 = actor (pi), 1 = critic (vf).
-constexpr int kW1F = 2 * 2 * 4 * 64;       // [net][ht][s][lane]           W1 * kTanhScale
-constexpr int kW2F = 2 * 2 * 2 * 16 * 64;  // [net][ot][kt][r/4][lane][4]  W2 * kTanhScale
-constexpr int oW1 = 0;
-constexpr int oW2 = oW1 + kW1F;
-constexpr int oB1 = oW2 + kW2F;            // [net][64]  b1 * kTanhScale
+// LDS image (floats).  net 0 = actor (pi), 1 = critic (vf).  An MFMA A fragment is 64 lanes x
+// 8 f16 = 256 floats (1 KiB), read with one ds_read_b128 per lane.
+constexpr int kFrag = 64 * 4;
+constexpr int oW1 = 0;                     // fragments [net][ht][m]          W1 * kTanhScale
+constexpr int oW2 = oW1 + 8 * kFrag;       // fragments [net][ot][c][hi/lo]   W2 * kTanhScale
+constexpr int oB1 = oW2 + 32 * kFrag;      // [net][64]  b1 * kTanhScale (fp32)
 constexpr int oB2 = oB1 + 2 * kHid;        // [net][64]  b2 * kTanhScale
 constexpr int oHA0 = oB2 + 2 * kHid;       // action_net.weight[0][64]
 constexpr int oHA1 = oHA0 + kHid;          // action_net.weight[1][64]
 constexpr int oHV = oHA1 + kHid;           // value_net.weight[0][64]
 constexpr int oSc = oHV + kHid;            // ba0 ba1 bv log_std0 log_std1 (+3 pad)
-constexpr int kPolicyLds = oSc + 8;        // 9,672 floats = 38.7 KB
+constexpr int kPolicyLds = oSc + 8;        // 10,696 floats = 42.8 KB
+
+// x = hi + lo: hi = x truncated to 11 significant bits (exact in f16 for 2^-14 <= |x| < 65504),
+// lo = f16(x - hi) (x - hi is exact).  Two values per v_cvt_pkrtz_f16_f32.
+__device__ __forceinline__ float hi11(float x) {
+    return __uint_as_float(__float_as_uint(x) & 0xFFFFE000u);
+}
+__device__ __forceinline__ uint32_t pk_rtz(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+// Weights (staged once per workgroup): hi rounded to nearest (ties away) on the integer bits.
+// Every conversion goes through these explicit integer ops and v_cvt_pkrtz, never a compiler
+// f32->f16 cast: hipcc lowers casts to v_cvt_f16_f32 or v_cvt_pk_f16_f32 depending on the
+// surrounding code, and the two kernels that share this image must stage the same bits.
+__device__ __forceinline__ float hi11_rn(float x) {
+    return __uint_as_float((__float_as_uint(x) + 0x1000u) & 0xFFFFE000u);
+}
+__device__ __forceinline__ _Float16 to_f16(float x) {
+    return __builtin_bit_cast(_Float16, (uint16_t)(pk_rtz(x, 0.0f) & 0xFFFFu));
+}
+template <class V>
+__device__ __forceinline__ void split8(const V &v, int base, h8 &hi, h8 &lo) {
+    u32x4 H, L;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const float x = v[base + 2 * p], y = v[base + 2 * p + 1];
+        const float xh = hi11(x), yh = hi11(y);
+        H[p] = pk_rtz(xh, yh);
+        L[p] = pk_rtz(x - xh, y - yh);
+    }
+    hi = __builtin_bit_cast(h8, H);
+    lo = __builtin_bit_cast(h8, L);
+}
 
 // Cooperative copy of the flat parameters into the LDS image (all threads of the block).
 __device__ __forceinline__ void stage_policy_weights(float *lds, const float *__restrict__ params,
                                                      int D, int tid, int nthreads) {
     const PLayout L(D);
-    for (int e = tid; e < kW1F; e += nthreads) {
-        const int lane = e & 63, s = (e >> 6) & 3, ht = (e >> 8) & 1, net = e >> 9;
-        const int row = 32 * ht + (lane & 31), col = 2 * s + (lane >> 5);
-        const int base = net ? L.vf0W : L.pi0W;
-        lds[oW1 + e] = col < D ? params[base + row * D + col] * kTanhScale : 0.0f;
+    _Float16 *fh = reinterpret_cast<_Float16 *>(lds);
+    // layer 1: fragment (net, ht, m), lane (r, hh), slot j -> W1[32 ht + r][j]
+    for (int e = tid; e < 8 * 64 * 8; e += nthreads) {
+        const int j = e & 7, lane = (e >> 3) & 63, m = (e >> 9) & 1, ht = (e >> 10) & 1,
+                  net = e >> 11;
+        const int row = 32 * ht + (lane & 31), hh = lane >> 5;
+        const float w = j < D ? params[(net ? L.vf0W : L.pi0W) + row * D + j] * kTanhScale : 0.0f;
+        const float whi = hi11_rn(w);
+        fh[2 * oW1 + e] = to_f16(m == 0 ? whi : (hh == 0 ? w - whi : 0.0f));
     }
-    for (int e = tid; e < kW2F; e += nthreads) {
-        const int q = e & 3, lane = (e >> 2) & 63, r4 = (e >> 8) & 3, kt = (e >> 10) & 1,
-                  ot = (e >> 11) & 1, net = e >> 12;
-        const int r = 4 * r4 + q;
-        const int row = 32 * ot + (lane & 31), col = 32 * kt + rho(r, lane >> 5);
-        lds[oW2 + e] = params[(net ? L.vf2W : L.pi2W) + row * kHid + col] * kTanhScale;
+    // layer 2: fragment (net, ot, c, hl), lane (r, hh), slot j -> W2[32 ot + r][k(c, hh, j)]
+    for (int e = tid; e < 32 * 64 * 8; e += nthreads) {
+        const int j = e & 7, lane = (e >> 3) & 63, hl = (e >> 9) & 1, c = (e >> 10) & 3,
+                  ot = (e >> 12) & 1, net = e >> 13;
+        const int row = 32 * ot + (lane & 31);
+        const int col = 32 * (c >> 1) + rho(8 * (c & 1) + j, lane >> 5);
+        const float w = params[(net ? L.vf2W : L.pi2W) + row * kHid + col] * kTanhScale;
+        const float whi = hi11_rn(w);
+        fh[2 * oW2 + e] = to_f16(hl == 0 ? whi : w - whi);
     }
     for (int e = tid; e < kHid; e += nthreads) {
         lds[oB1 + e] = params[L.pi0b + e] * kTanhScale;
@@ -117,6 +172,14 @@ __device__ __forceinline__ float tanh_s(float y) {
     return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
 }
 
+// Layer-1 B operand of a lane from its agent's observation row o[0..8) (zero-padded past D):
+// half 0 carries the hi parts, half 1 the lo parts (see the mapping above).
+__device__ __forceinline__ h8 obs_operand(const float (&o)[8], int h) {
+    h8 hi, lo;
+    split8(o, 0, hi, lo);
+    return h == 0 ? hi : lo;
+}
+
 // accumulator <- bias rows rho(reg, h) of hidden rows [32*ht, 32*ht + 32): 4 x ds_read_b128
 __device__ __forceinline__ f32x16 bias_acc(const float *b, int ht, int h) {
     f32x16 a;
@@ -131,45 +194,52 @@ __device__ __forceinline__ f32x16 bias_acc(const float *b, int ht, int h) {
     return a;
 }
 
+__device__ __forceinline__ f32x16 mma16(const h8 &a, const h8 &b, const f32x16 &c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
 // One network (net 0 actor / 1 critic) over one 32-agent tile: layer 1, tanh, layer 2, tanh.
 // Leaves tanh(H2) rows rho(reg, h) (+32*ot) of agent l&31 in c0 (ot 0) and c1 (ot 1).
-__device__ __forceinline__ void net_tile(const float *lds, int net, const float (&ob)[4], int D,
-                                         int lane, int h, f32x16 &c0, f32x16 &c1) {
+__device__ __forceinline__ void net_tile(const float *lds, int net, const h8 &bo, int lane, int h,
+                                         f32x16 &c0, f32x16 &c1) {
+    const h8 *fr = reinterpret_cast<const h8 *>(lds) + lane;  // fragment f: fr[64 f]
     f32x16 a0 = bias_acc(lds + oB1 + net * kHid, 0, h);
     f32x16 a1 = bias_acc(lds + oB1 + net * kHid, 1, h);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        if (2 * s >= D) break;
-        a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + ((net * 2 + 0) * 4 + s) * 64 + lane],
-                                                  ob[s], a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[oW1 + ((net * 2 + 1) * 4 + s) * 64 + lane],
-                                                  ob[s], a1, 0, 0, 0);
+    {
+        const int f1 = oW1 / kFrag + net * 4;
+        a0 = mma16(fr[64 * (f1 + 0)], bo, a0);
+        a1 = mma16(fr[64 * (f1 + 2)], bo, a1);
+        a0 = mma16(fr[64 * (f1 + 1)], bo, a0);
+        a1 = mma16(fr[64 * (f1 + 3)], bo, a1);
     }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         a0[reg] = tanh_s(a0[reg]);
         a1[reg] = tanh_s(a1[reg]);
     }
+    h8 bh[4], bl[4];
+    split8(a0, 0, bh[0], bl[0]);
+    split8(a0, 8, bh[1], bl[1]);
+    split8(a1, 0, bh[2], bl[2]);
+    split8(a1, 8, bh[3], bl[3]);
     c0 = bias_acc(lds + oB2 + net * kHid, 0, h);
     c1 = bias_acc(lds + oB2 + net * kHid, 1, h);
 #if FENV_POLICY_PRIO
     __builtin_amdgcn_s_setprio(1);  // a wave in its MFMA phase wins issue arbitration
 #endif
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-            const f32x4 w0 = *reinterpret_cast<const f32x4 *>(
-                &lds[oW2 + ((((net * 2 + 0) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
-            const f32x4 w1 = *reinterpret_cast<const f32x4 *>(
-                &lds[oW2 + ((((net * 2 + 1) * 2 + kt) * 4 + r4) * 64 + lane) * 4]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float b = kt == 0 ? a0[4 * r4 + q] : a1[4 * r4 + q];
-                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[q], b, c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[q], b, c1, 0, 0, 0);
-            }
-        }
+    for (int c = 0; c < 4; ++c) {
+        const int f0 = oW2 / kFrag + ((net * 2 + 0) * 4 + c) * 2;
+        const int f1 = oW2 / kFrag + ((net * 2 + 1) * 4 + c) * 2;
+        const h8 w0h = fr[64 * f0], w0l = fr[64 * (f0 + 1)];
+        const h8 w1h = fr[64 * f1], w1l = fr[64 * (f1 + 1)];
+        // small terms first
+        c0 = mma16(w0h, bl[c], c0);
+        c1 = mma16(w1h, bl[c], c1);
+        c0 = mma16(w0l, bh[c], c0);
+        c1 = mma16(w1l, bh[c], c1);
+        c0 = mma16(w0h, bh[c], c0);
+        c1 = mma16(w1h, bh[c], c1);
     }
 #if FENV_POLICY_PRIO
     __builtin_amdgcn_s_setprio(0);
@@ -224,10 +294,9 @@ struct PolicyLane {
     float logp;   // sum over both components of Normal(mu, std).log_prob(act) (both halves)
 };
 
-// Full policy evaluation of one 32-agent tile.  ob[s] = obs[agent][2s + h] (0 for 2s+h >= D);
+// Full policy evaluation of one 32-agent tile.  bo = obs_operand(agent's observation row, h);
 // `row` is the agent's row in the batch (Philox counter); value_only skips the actor.
-__device__ __forceinline__ PolicyLane policy_tile(const float *lds, const float (&ob)[4], int D,
-                                                  int lane, int64_t row, uint64_t seed,
+__device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo, int lane, int64_t row, uint64_t seed,
                                                   uint64_t offset, bool deterministic,
                                                   bool value_only) {
     const int h = lane >> 5;
@@ -235,7 +304,7 @@ __device__ __forceinline__ PolicyLane policy_tile(const float *lds, const float 
     f32x16 c0, c1;
     float pa = 0.0f;
     if (!value_only) {
-        net_tile(lds, 0, ob, D, lane, h, c0, c1);
+        net_tile(lds, 0, bo, lane, h, c0, c1);
         const float p0 = head_dot(lds + oHA0, c0, c1, h);
         const float p1 = head_dot(lds + oHA1, c0, c1, h);
         // keep component h: own partial + the partner half's partial of the same component
@@ -243,7 +312,7 @@ __device__ __forceinline__ PolicyLane policy_tile(const float *lds, const float 
         pa = h == 0 ? p0 + other : other + p1;
     }
     __builtin_amdgcn_sched_barrier(0);  // actor, then critic: overlapping them costs registers
-    net_tile(lds, 1, ob, D, lane, h, c0, c1);
+    net_tile(lds, 1, bo, lane, h, c0, c1);
     o.value = join_halves(head_dot(lds + oHV, c0, c1, h), h) + lds[oSc + 2];
     if (value_only) {
         o.mu = o.act = o.clip = o.logp = 0.0f;

@@ -33,14 +33,11 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
         asm volatile("" ::: "memory");  // no hoisting of the LDS weight image into registers
         const int64_t row = tile * 32 + j;
         const bool valid = row < B;
-        float ob[4];
+        float o[8];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int col = 2 * s + h;
-            ob[s] = (valid && col < D) ? obs[row * D + col] : 0.0f;
-        }
-        const PolicyLane r = policy_tile(lds, ob, D, lane, row, seed, offset, deterministic != 0,
-                                         value_only);
+        for (int col = 0; col < 8; ++col) o[col] = (valid && col < D) ? obs[row * D + col] : 0.0f;
+        const PolicyLane r = policy_tile(lds, obs_operand(o, h), lane, row, seed, offset,
+                                         deterministic != 0, value_only);
         if (valid) {
             if (mu_out) mu_out[row * 2 + h] = r.mu;
             if (act_out) act_out[row * 2 + h] = r.act;

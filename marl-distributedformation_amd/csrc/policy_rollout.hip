@@ -14,15 +14,16 @@
 // observations[k] and the MFMA B operands come from the same slice), the policy outputs are
 // staged in the same slice (coalesced stores of mu/action/clipped/value/log_prob, and the lane
 // that owns agent l picks up its clipped action), then the env step runs on registers.
-// 4 waves per workgroup share one 38.7 KB weight image (46.7 KB of LDS with the stage slices:
-// 3 workgroups per CU); <= 128 VGPRs.  A wave in its MFMA phase raises its issue priority
+// 4 waves per workgroup share one 42.8 KB weight image (50.8 KB of LDS with the stage slices:
+// 3 workgroups per CU).  A wave in its MFMA phase raises its issue priority
 // (s_setprio) so the VALU/LDS work of the other waves fills around it.  Measured against 8-wave
 // workgroups with and without the priority (build_variants, tools/gpu_policy.sh): 4 waves +
 // priority is +9 % at F = 65,536 x 10 and +2 % at F = 262,144 x 10.
 // GAE runs as one short HBM-bound launch after it (k_gae: 17 B per agent-step, ~2 % of the
 // rollout; holding T rewards and values in registers would cost the occupancy).
 //
-// Roofline: MFMA fp32 (18,816 FLOP per agent-step + 9,344 per agent for the last value);
+// Work: 18,816 fp32-equivalent FLOP per agent-step (+9,344 per agent for the last value) as
+// split-f16 MFMAs (policy_device.h), plus ~256 tanh per agent-step on the VALU;
 // HBM output is ~78 B per agent-step, an order of magnitude below the MFMA time.
 #pragma clang fp contract(off)
 
@@ -40,9 +41,10 @@ namespace fenvk {
 #define FENV_PR_WAVES 4
 #endif
 constexpr int kPRWaves = FENV_PR_WAVES;
-// <= 128 VGPRs per wave
+// LDS (50.8 KB per 4-wave workgroup) allows 3 workgroups = 3 waves per SIMD, so the register
+// budget is 168 VGPRs; the compiler is told so (at a 128 budget it spills)
 #ifndef FENV_PR_OCCUPANCY
-#define FENV_PR_OCCUPANCY __attribute__((amdgpu_waves_per_eu(4)))
+#define FENV_PR_OCCUPANCY __attribute__((amdgpu_waves_per_eu(3)))
 #endif
 constexpr size_t kPRLdsBytes = (size_t)(kPolicyLds + kPRWaves * 512) * sizeof(float);
 static_assert(kPolicyLds % 4 == 0, "stage slices must stay 16-byte aligned");
@@ -61,16 +63,16 @@ __device__ __forceinline__ void store_span(const float *stage, int nf, float *ds
     }
 }
 
-// The MFMA B operands of the wave's two tiles from the staged observation rows.
+// The layer-1 MFMA B operands of the wave's two tiles from the staged observation rows.
 template <int D>
-__device__ __forceinline__ void tile_operands(const float *stage, int j, int h, float (&ob)[2][4]) {
+__device__ __forceinline__ void tile_operands(const float *stage, int j, int h, h8 (&bo)[2]) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+        float o[8];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int col = 2 * s + h;
-            ob[t][s] = col < D ? stage[(32 * t + j) * D + col] : 0.0f;
-        }
+        for (int col = 0; col < 8; ++col) o[col] = col < D ? stage[(32 * t + j) * D + col] : 0.0f;
+        bo[t] = obs_operand(o, h);
+    }
 }
 
 template <int D, int MODE>
@@ -132,15 +134,15 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         const int64_t rk = (int64_t)k * A;
         // the observation the action is taken on -> observations[k]
         store_obs_rows<D>(stage, o, ln, M, b.obs + (rk + a_first) * D);
-        float ob[2][4];
-        tile_operands<D>(stage, j, h, ob);
+        h8 bo[2];
+        tile_operands<D>(stage, j, h, bo);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             // one tile at a time, outputs parked in LDS at once (keeps the step under 128 VGPRs)
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            const PolicyLane pl = policy_tile(wimg, ob[t], D, ln, a_first + 32 * t + j, g.seed,
+            const PolicyLane pl = policy_tile(wimg, bo[t], ln, a_first + 32 * t + j, g.seed,
                                               g.offset + k, det, false);
             const int r = 32 * t + j;
             stage[2 * r + h] = pl.mu;
@@ -184,14 +186,14 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
     float lv = 0.0f;
     if (b.last_value) {
         const int j = lane & 31, h = lane >> 5;
-        float ob[2][4];
-        tile_operands<D>(stage, j, h, ob);
+        h8 bo[2];
+        tile_operands<D>(stage, j, h, bo);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            const PolicyLane pv = policy_tile(wimg, ob[t], D, lane, 0, 0, 0, true, true);
+            const PolicyLane pv = policy_tile(wimg, bo[t], lane, 0, 0, 0, true, true);
             if (h == 0) stage[384 + 32 * t + j] = pv.value;
         }
         __builtin_amdgcn_wave_barrier();
