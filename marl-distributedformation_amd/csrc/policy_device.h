@@ -33,8 +33,9 @@
 // (SURVEY §8(a) R10).
 //
 // tanh.  Hidden-layer weights and biases are staged pre-multiplied by 2/ln2, so an accumulator
-// holds y = 2x*log2(e) and tanh(x) = 1 - 2 / (1 + 2^y): v_exp_f32, v_add, v_rcp_f32, v_fma.
-// |abs err| < 5e-7.
+// holds y = 2x*log2(e); the layers pass on r = 1/(1 + 2^y) = (1 - tanh x)/2 (v_exp_f32, v_add,
+// v_rcp_f32) and the consumers fold tanh = 1 - 2r into their weights and biases (see rsig).
+// |abs err of tanh| < 5e-7.
 #pragma once
 #pragma clang fp contract(off)
 
@@ -83,13 +84,13 @@ struct PLayout {
 // 8 f16 = 256 floats (1 KiB), read with one ds_read_b128 per lane.
 constexpr int kFrag = 64 * 4;
 constexpr int oW1 = 0;                     // fragments [net][ht][m]          W1 * kTanhScale
-constexpr int oW2 = oW1 + 8 * kFrag;       // fragments [net][ot][c][hi/lo]   W2 * kTanhScale
+constexpr int oW2 = oW1 + 8 * kFrag;       // fragments [net][ot][c][hi/lo]   -2 * W2 * kTanhScale
 constexpr int oB1 = oW2 + 32 * kFrag;      // [net][64]  b1 * kTanhScale (fp32)
-constexpr int oB2 = oB1 + 2 * kHid;        // [net][64]  b2 * kTanhScale
-constexpr int oHA0 = oB2 + 2 * kHid;       // action_net.weight[0][64]
-constexpr int oHA1 = oHA0 + kHid;          // action_net.weight[1][64]
-constexpr int oHV = oHA1 + kHid;           // value_net.weight[0][64]
-constexpr int oSc = oHV + kHid;            // ba0 ba1 bv log_std0 log_std1 (+3 pad)
+constexpr int oB2 = oB1 + 2 * kHid;        // [net][64]  (b2 + rowsum W2) * kTanhScale
+constexpr int oHA0 = oB2 + 2 * kHid;       // -2 * action_net.weight[0][64]
+constexpr int oHA1 = oHA0 + kHid;          // -2 * action_net.weight[1][64]
+constexpr int oHV = oHA1 + kHid;           // -2 * value_net.weight[0][64]
+constexpr int oSc = oHV + kHid;            // ba0 ba1 bv (each + rowsum) log_std0 log_std1 (+3)
 constexpr int kPolicyLds = oSc + 8;        // 10,696 floats = 42.8 KB
 
 // x = hi + lo: hi = x truncated to 11 significant bits (exact in f16 for 2^-14 <= |x| < 65504),
@@ -144,32 +145,42 @@ __device__ __forceinline__ void stage_policy_weights(float *lds, const float *__
                   ot = (e >> 12) & 1, net = e >> 13;
         const int row = 32 * ot + (lane & 31);
         const int col = 32 * (c >> 1) + rho(8 * (c & 1) + j, lane >> 5);
-        const float w = params[(net ? L.vf2W : L.pi2W) + row * kHid + col] * kTanhScale;
+        const float w = -2.0f * (params[(net ? L.vf2W : L.pi2W) + row * kHid + col] * kTanhScale);
         const float whi = hi11_rn(w);
         fh[2 * oW2 + e] = to_f16(hl == 0 ? whi : w - whi);
     }
+    // layers fed with r = (1 - tanh) / 2 (see rsig): W.tanh + b = (b + rowsum W) - 2 W.r
+    for (int e = tid; e < 2 * kHid; e += nthreads) {
+        const int net = e >> 6, row = e & 63;
+        lds[oB1 + e] = params[(net ? L.vf0b : L.pi0b) + row] * kTanhScale;
+        const float *w2 = params + (net ? L.vf2W : L.pi2W) + row * kHid;
+        float sum = params[(net ? L.vf2b : L.pi2b) + row] * kTanhScale;
+        for (int k = 0; k < kHid; ++k) sum += w2[k] * kTanhScale;
+        lds[oB2 + e] = sum;
+    }
     for (int e = tid; e < kHid; e += nthreads) {
-        lds[oB1 + e] = params[L.pi0b + e] * kTanhScale;
-        lds[oB1 + kHid + e] = params[L.vf0b + e] * kTanhScale;
-        lds[oB2 + e] = params[L.pi2b + e] * kTanhScale;
-        lds[oB2 + kHid + e] = params[L.vf2b + e] * kTanhScale;
-        lds[oHA0 + e] = params[L.actW + e];
-        lds[oHA1 + e] = params[L.actW + kHid + e];
-        lds[oHV + e] = params[L.valW + e];
+        lds[oHA0 + e] = -2.0f * params[L.actW + e];
+        lds[oHA1 + e] = -2.0f * params[L.actW + kHid + e];
+        lds[oHV + e] = -2.0f * params[L.valW + e];
     }
     if (tid < 8) {
         float v = 0.0f;
-        if (tid < 2) v = params[L.actb + tid];
-        else if (tid == 2) v = params[L.valb];
-        else if (tid < 5) v = params[L.logstd + tid - 3];
+        if (tid < 3) {  // head biases + rowsum of the head weights
+            const float *w = params + (tid < 2 ? L.actW + tid * kHid : L.valW);
+            v = params[tid < 2 ? L.actb + tid : L.valb];
+            for (int k = 0; k < kHid; ++k) v += w[k];
+        } else if (tid < 5) {
+            v = params[L.logstd + tid - 3];
+        }
         lds[oSc + tid] = v;
     }
 }
 
-// tanh(x) from y = x * 2/ln2 (see header)
-__device__ __forceinline__ float tanh_s(float y) {
-    const float e = __builtin_amdgcn_exp2f(y);
-    return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
+// r = 1 / (1 + 2^y) = (1 - tanh(x)) / 2 for y = x * 2/ln2: v_exp_f32, v_add, v_rcp_f32.  The
+// hidden layers hand r on instead of tanh = 1 - 2r; the next layer and the heads absorb the
+// affine map (weights -2W, bias b + rowsum W, staged above), which saves the v_fma per unit.
+__device__ __forceinline__ float rsig(float y) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y));
 }
 
 // Layer-1 B operand of a lane from its agent's observation row o[0..8) (zero-padded past D):
@@ -199,7 +210,8 @@ __device__ __forceinline__ f32x16 mma16(const h8 &a, const h8 &b, const f32x16 &
 }
 
 // One network (net 0 actor / 1 critic) over one 32-agent tile: layer 1, tanh, layer 2, tanh.
-// Leaves tanh(H2) rows rho(reg, h) (+32*ot) of agent l&31 in c0 (ot 0) and c1 (ot 1).
+// Leaves r(H2) = (1 - tanh(H2)) / 2, rows rho(reg, h) (+32*ot) of agent l&31, in c0 (ot 0) and
+// c1 (ot 1).
 __device__ __forceinline__ void net_tile(const float *lds, int net, const h8 &bo, int lane, int h,
                                          f32x16 &c0, f32x16 &c1) {
     const h8 *fr = reinterpret_cast<const h8 *>(lds) + lane;  // fragment f: fr[64 f]
@@ -214,8 +226,8 @@ __device__ __forceinline__ void net_tile(const float *lds, int net, const h8 &bo
     }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-        a0[reg] = tanh_s(a0[reg]);
-        a1[reg] = tanh_s(a1[reg]);
+        a0[reg] = rsig(a0[reg]);
+        a1[reg] = rsig(a1[reg]);
     }
     h8 bh[4], bl[4];
     split8(a0, 0, bh[0], bl[0]);
@@ -246,8 +258,8 @@ __device__ __forceinline__ void net_tile(const float *lds, int net, const h8 &bo
 #endif
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-        c0[reg] = tanh_s(c0[reg]);
-        c1[reg] = tanh_s(c1[reg]);
+        c0[reg] = rsig(c0[reg]);
+        c1[reg] = rsig(c1[reg]);
     }
 }
 

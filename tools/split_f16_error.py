@@ -1,6 +1,8 @@
 """Numerical justification of the split-f16 policy MFMA (csrc/policy_device.h), on the CPU.
 
-Emulates exactly what the kernel computes for every fp32 product w*x of the two hidden layers:
+Emulates what the kernel computes.  The hidden layers carry r = 1/(1 + e^{2x}) instead of
+tanh(x) = 1 - 2r (the next layer and the heads absorb the affine map: weights -2W, bias
+b + rowsum W), and every fp32 product w*x of the two hidden layers is split:
     weights      w*2/ln2 -> hi = nearest 11-significant-bit value (ties away), lo = rtz_f16(w - hi)
     activations  x       -> hi = x truncated to 11 significant bits,      lo = rtz_f16(x - hi)
     product      hi_w*hi_x + hi_w*lo_x + lo_w*hi_x   (each exact, accumulated in fp32 -- here f64)
@@ -58,21 +60,37 @@ def lin(W, b, x, ftz):
     return (xh @ wh.T + xl @ wh.T + xh @ wl.T + bk).astype(np.float32)
 
 
-def tanh_s(y):
+def rsig(y):
+    """r = 1 / (1 + 2^y), so tanh(x) = 1 - 2 r for y = x * 2/ln2 (v_exp_f32, v_add, v_rcp_f32)."""
     with np.errstate(over="ignore"):
         e = np.exp2(y.astype(np.float64)).astype(np.float32)
-    return np.float32(1) - np.float32(2) / (np.float32(1) + e)
+    return (np.float32(1) / (np.float32(1) + e)).astype(np.float32)
+
+
+def lin_r(W, b, r, ftz):
+    """Layer fed with r instead of tanh = 1 - 2r: W.(1 - 2r) + b = (b + rowsum W) - 2 W.r."""
+    Wk = (W * K).astype(np.float32)
+    bk = (b * K).astype(np.float32) + Wk.sum(axis=1, dtype=np.float32)
+    W2 = (np.float32(-2) * Wk).astype(np.float32)
+    wh, wl = split(W2, True, ftz)
+    xh, xl = split(r, False, ftz)
+    return (xh @ wh.T + xl @ wh.T + xh @ wl.T + bk).astype(np.float32)
+
+
+def head_r(W, b, r):
+    bb = (b + W.sum(axis=1, dtype=np.float32)).astype(np.float32)
+    return (r.astype(np.float64) @ (np.float32(-2) * W).T.astype(np.float64) + bb).astype(np.float32)
 
 
 def forward(sd, obs, ftz=False):
     g = {k: v.numpy() for k, v in sd.items()}
-    h = tanh_s(lin(g["mlp_extractor.policy_net.0.weight"], g["mlp_extractor.policy_net.0.bias"], obs, ftz))
-    h = tanh_s(lin(g["mlp_extractor.policy_net.2.weight"], g["mlp_extractor.policy_net.2.bias"], h, ftz))
-    v = tanh_s(lin(g["mlp_extractor.value_net.0.weight"], g["mlp_extractor.value_net.0.bias"], obs, ftz))
-    v = tanh_s(lin(g["mlp_extractor.value_net.2.weight"], g["mlp_extractor.value_net.2.bias"], v, ftz))
-    mu = h.astype(np.float64) @ g["action_net.weight"].T.astype(np.float64) + g["action_net.bias"]
-    val = v.astype(np.float64) @ g["value_net.weight"].T.astype(np.float64) + g["value_net.bias"]
-    return mu.astype(np.float32), val[:, 0].astype(np.float32)
+    h = rsig(lin(g["mlp_extractor.policy_net.0.weight"], g["mlp_extractor.policy_net.0.bias"], obs, ftz))
+    h = rsig(lin_r(g["mlp_extractor.policy_net.2.weight"], g["mlp_extractor.policy_net.2.bias"], h, ftz))
+    v = rsig(lin(g["mlp_extractor.value_net.0.weight"], g["mlp_extractor.value_net.0.bias"], obs, ftz))
+    v = rsig(lin_r(g["mlp_extractor.value_net.2.weight"], g["mlp_extractor.value_net.2.bias"], v, ftz))
+    mu = head_r(g["action_net.weight"], g["action_net.bias"], h)
+    val = head_r(g["value_net.weight"], g["value_net.bias"], v)
+    return mu, val[:, 0]
 
 
 def make_policy(D, seed):
