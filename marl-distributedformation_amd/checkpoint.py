@@ -1,0 +1,182 @@
+"""SB3-layout checkpoint zips: save, load and the CheckpointCallback schedule.
+
+The reference trains with ``CheckpointCallback(save_freq=10, save_path=f'{this_dir}/logs/{cfg.name}/')``
+(vectorized_env.py:124) and plays back the newest ``rl_model_{num_timesteps}_steps.zip``
+(visualize_policy.py:29-35) through ``PPO.load``.  stable-baselines3 is not installed here, so
+this module writes and reads the SB3 2.x ``save_to_zip_file`` layout itself:
+
+    data                        JSON: the model's hyper-parameters / counters
+    policy.pth                  torch.save(policy.state_dict())  (SB3 parameter names)
+    policy.optimizer.pth        torch.save(Adam.state_dict()) over the 13 SB3 tensors
+    pytorch_variables.pth       torch.save({})
+    _stable_baselines3_version  text
+    system_info.txt             text
+
+Loading reads ``policy.pth`` with ``torch.load(weights_only=True)`` only (no pickle
+execution), so zips written by real SB3 load here too.  Zips written here carry the same entry
+names and tensors; SB3's ``data`` entries for ``policy_class``, ``observation_space`` and
+``action_space`` are cloudpickled gymnasium/SB3 objects that cannot be produced without those
+packages, so an SB3 ``PPO.load`` of them needs ``custom_objects`` for those three keys
+(INTEGRATION.md).  Parity against SB3 itself: unpinned (SB3 absent).
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+import platform
+import zipfile
+
+import torch
+
+SB3_VERSION = "2.3.2"  # the version string written into _stable_baselines3_version
+
+# SB3 ActorCriticPolicy.parameters() order (own Parameter first, then submodules): the index
+# order of the optimizer state.  Names as in include/fenv.h / policy.PARAM_SPECS.
+SB3_PARAM_ORDER = [
+    "log_std",
+    "mlp_extractor.policy_net.0.weight", "mlp_extractor.policy_net.0.bias",
+    "mlp_extractor.policy_net.2.weight", "mlp_extractor.policy_net.2.bias",
+    "mlp_extractor.value_net.0.weight", "mlp_extractor.value_net.0.bias",
+    "mlp_extractor.value_net.2.weight", "mlp_extractor.value_net.2.bias",
+    "action_net.weight", "action_net.bias",
+    "value_net.weight", "value_net.bias",
+]
+
+# keys of SB3's saved ``data`` whose values are pickled objects (need custom_objects in SB3)
+_OPAQUE = {"policy_class": "<class 'stable_baselines3.common.policies.ActorCriticPolicy'>",
+           "observation_space": "<class 'gymnasium.spaces.box.Box'>",
+           "action_space": "<class 'gymnasium.spaces.box.Box'>"}
+
+
+def _tensor_bytes(obj) -> bytes:
+    buf = io.BytesIO()
+    torch.save(obj, buf)
+    return buf.getvalue()
+
+
+def _state_to_cpu(sd: dict) -> dict:
+    return {k: torch.as_tensor(v).detach().to("cpu", torch.float32).clone() for k, v in sd.items()}
+
+
+def optimizer_state_from_flat(shapes: list[tuple[str, tuple]], opt_state: dict) -> dict:
+    """Re-express a torch Adam state over ONE flat parameter (ppo.PPO) as SB3's Adam state over
+    the 13 policy tensors (same step count and moments, sliced per tensor)."""
+    st = opt_state.get("state", {}).get(0, {})
+    groups = opt_state.get("param_groups", [{}])
+    offs, o = {}, 0
+    for name, shp in shapes:
+        n = 1
+        for s in shp:
+            n *= int(s)
+        offs[name] = (o, n, tuple(shp))
+        o += n
+    state = {}
+    for i, name in enumerate(SB3_PARAM_ORDER):
+        if not st:
+            break
+        a, n, shp = offs[name]
+        state[i] = {"step": torch.as_tensor(st["step"]).detach().cpu().clone(),
+                    "exp_avg": st["exp_avg"][a:a + n].detach().cpu().reshape(shp).clone(),
+                    "exp_avg_sq": st["exp_avg_sq"][a:a + n].detach().cpu().reshape(shp).clone()}
+    g = {k: v for k, v in groups[0].items() if k != "params"}
+    g["params"] = list(range(len(SB3_PARAM_ORDER)))
+    return {"state": state, "param_groups": [g]}
+
+
+def save_sb3_zip(path: str, state_dict: dict, *, num_timesteps: int, data: dict | None = None,
+                 optimizer_state: dict | None = None) -> str:
+    """Write an SB3-layout model zip; returns ``path`` (".zip" appended if missing, as SB3)."""
+    if not path.endswith(".zip"):
+        path += ".zip"
+    missing = [k for k in SB3_PARAM_ORDER if k not in state_dict]
+    if missing:
+        raise KeyError(f"state_dict lacks SB3 parameters {missing}")
+    d = {k: {":type:": t, ":serialized:": ""} for k, t in _OPAQUE.items()}
+    d.update({"num_timesteps": int(num_timesteps), "_total_timesteps": int(num_timesteps)})
+    d.update(data or {})
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = path + ".tmp"
+    with zipfile.ZipFile(tmp, "w") as z:
+        z.writestr("data", json.dumps(d, indent=4, sort_keys=False))
+        z.writestr("policy.pth", _tensor_bytes(_state_to_cpu(state_dict)))
+        if optimizer_state is not None:
+            z.writestr("policy.optimizer.pth", _tensor_bytes(optimizer_state))
+        z.writestr("pytorch_variables.pth", _tensor_bytes({}))
+        z.writestr("_stable_baselines3_version", SB3_VERSION)
+        z.writestr("system_info.txt",
+                   f"- OS: {platform.platform()}\n- Python: {platform.python_version()}\n"
+                   f"- PyTorch: {torch.__version__}\n- Stable-Baselines3: {SB3_VERSION}\n")
+    os.replace(tmp, path)
+    return path
+
+
+def load_sb3_zip(path: str) -> tuple[dict, dict]:
+    """(policy state_dict on CPU, data dict) from an SB3 model zip -- ours or SB3's.
+
+    Only ``policy.pth`` is deserialised, with ``torch.load(weights_only=True)``; ``data`` is
+    parsed as JSON and pickled entries are left as their JSON stubs."""
+    with zipfile.ZipFile(path) as z:
+        names = set(z.namelist())
+        if "policy.pth" not in names:
+            raise ValueError(f"{path}: no policy.pth (not an SB3 model zip)")
+        sd = torch.load(io.BytesIO(z.read("policy.pth")), map_location="cpu", weights_only=True)
+        data = json.loads(z.read("data").decode()) if "data" in names else {}
+    return dict(sd), data
+
+
+def checkpoint_name(num_timesteps: int, prefix: str = "rl_model") -> str:
+    """SB3 CheckpointCallback file name: ``{prefix}_{num_timesteps}_steps.zip``."""
+    return f"{prefix}_{int(num_timesteps)}_steps.zip"
+
+
+def latest_checkpoint(directory: str) -> str:
+    """The newest checkpoint in ``directory``, chosen as visualize_policy.py:33-34 does: among the
+    files whose name contains "rl_model", the one with the largest ``int(name.split("_")[-2])``."""
+    files = [f for f in os.listdir(directory) if "rl_model" in f]
+    if not files:
+        raise FileNotFoundError(f"no rl_model_*_steps.zip in {directory}")
+    return os.path.join(directory, max(files, key=lambda x: int(x.split("_")[-2].split(".")[0])))
+
+
+class CheckpointCallback:
+    """SB3 ``CheckpointCallback(save_freq, save_path, name_prefix="rl_model")``.
+
+    SB3 calls ``_on_step`` once per vectorised env step inside ``collect_rollouts`` and saves
+    whenever ``n_calls % save_freq == 0``, naming the file by the model's ``num_timesteps`` at that
+    moment (already counting that step).  :meth:`on_steps` replays that schedule for a rollout of
+    ``n`` env steps collected in one launch; the fused collector only exposes the policy at the
+    rollout boundary, so every save due inside a rollout is written at its end with that step's
+    ``num_timesteps`` (with the reference's save_freq=10 = n_steps the two coincide)."""
+
+    def __init__(self, save_freq: int, save_path: str, name_prefix: str = "rl_model",
+                 verbose: int = 0):
+        if save_freq < 1:
+            raise ValueError("save_freq must be >= 1")
+        self.save_freq = int(save_freq)
+        self.save_path = save_path
+        self.name_prefix = name_prefix
+        self.verbose = verbose
+        self.n_calls = 0
+        self.saved: list[str] = []
+
+    def on_steps(self, model, n: int, num_envs: int) -> list[str]:
+        """Advance by a rollout of ``n`` env steps of ``num_envs`` agents that has just been
+        collected (``model.num_timesteps`` already counts it); save as SB3 would have."""
+        out = []
+        t_end = int(model.num_timesteps)
+        for s in range(1, int(n) + 1):
+            self.n_calls += 1
+            if self.n_calls % self.save_freq == 0:
+                out.append(self._save(model, t_end - (int(n) - s) * int(num_envs)))
+        return out
+
+    def _save(self, model, num_timesteps: int) -> str:
+        path = os.path.join(self.save_path, checkpoint_name(num_timesteps, self.name_prefix))
+        model.save(path, num_timesteps=num_timesteps)
+        self.saved.append(path)
+        if self.verbose:
+            print(f"Saving model checkpoint to {path}")
+        return path
+
+    __call__ = on_steps

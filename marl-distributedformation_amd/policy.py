@@ -99,6 +99,17 @@ class MlpPolicy:
                 raise ValueError(f"{k}: shape {tuple(t.shape)} != {tuple(v.shape)}")
             v.copy_(t)
 
+    @classmethod
+    def from_checkpoint(cls, path: str, device=None) -> "MlpPolicy":
+        """Policy from an SB3 model zip (``rl_model_*_steps.zip``, ours or SB3's; only its
+        ``policy.pth`` is read, with torch.load(weights_only=True)): visualize_policy.py:35."""
+        from .checkpoint import load_sb3_zip
+        sd, _ = load_sb3_zip(path)
+        D = int(sd["mlp_extractor.policy_net.0.weight"].shape[1])
+        pol = cls(D, device=device)
+        pol.load_state_dict(sd)
+        return pol
+
     def parameters_flat(self) -> torch.Tensor:
         return self.flat
 

@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as Fn
 
+from . import checkpoint as ckpt
 from .policy import MlpPolicy
 from .rollout import RolloutBuffer, RolloutCollector
 
@@ -72,6 +73,7 @@ class PPO:
 
     def __init__(self, env, cfg: PPOConfig | None = None, seed: int = 0, policy=None):
         self.cfg = cfg or PPOConfig()
+        self.seed = int(seed)
         self.env = env
         self.policy = policy or MlpPolicy(env.obs_dim, device=env.device, seed=seed)
         self.buffer = RolloutBuffer(self.cfg.n_steps, env.num_envs, env.obs_dim, env.device,
@@ -121,11 +123,54 @@ class PPO:
         return self.stats
 
     def learn(self, total_timesteps: int, callback=None) -> "PPO":
-        """SB3 ``learn``: alternate collect_rollouts and train until total_timesteps."""
+        """SB3 ``learn``: alternate collect_rollouts and train until total_timesteps.
+
+        ``callback`` is a :class:`checkpoint.CheckpointCallback` (run after each collection, as
+        SB3 runs its ``_on_step`` inside ``collect_rollouts``; only rank 0 writes), a plain
+        function ``f(ppo)`` called after each train (returning False stops), or a list of both."""
+        cbs = callback if isinstance(callback, (list, tuple)) else [callback]
+        rank = dist.get_rank() if self.world > 1 else 0
         while self.num_timesteps < total_timesteps:
             with torch.no_grad():
                 self.collector.collect()
+            for cb in cbs:
+                if hasattr(cb, "on_steps") and rank == 0:
+                    cb.on_steps(self, self.cfg.n_steps, self.env.num_envs * self.world)
             self.train()
-            if callback is not None and callback(self) is False:
+            stop = False
+            for cb in cbs:
+                if cb is not None and not hasattr(cb, "on_steps") and cb(self) is False:
+                    stop = True
+            if stop:
                 break
         return self
+
+    # ---------------------------------------------------------------- SB3 model zips
+    def hyperparameters(self) -> dict:
+        c = self.cfg
+        return {"n_steps": c.n_steps, "learning_rate": c.learning_rate, "ent_coef": c.ent_coef,
+                "n_epochs": c.n_epochs, "batch_size": c.batch_size, "gamma": c.gamma,
+                "gae_lambda": c.gae_lambda, "clip_range": c.clip_range, "vf_coef": c.vf_coef,
+                "max_grad_norm": c.max_grad_norm, "normalize_advantage": c.normalize_advantage,
+                "n_envs": self.env.num_envs * self.world, "seed": self.seed}
+
+    def save(self, path: str, num_timesteps: int | None = None) -> str:
+        """SB3 ``model.save(path)``: an SB3-layout zip (checkpoint.py) with the policy's SB3
+        state_dict, the Adam state re-expressed per SB3 tensor, and the hyper-parameters."""
+        t = self.num_timesteps if num_timesteps is None else int(num_timesteps)
+        opt = ckpt.optimizer_state_from_flat(self.policy.param_shapes(), self.opt.state_dict())
+        return ckpt.save_sb3_zip(path, self.policy.state_dict(), num_timesteps=t,
+                                 data=self.hyperparameters(), optimizer_state=opt)
+
+    @classmethod
+    def load(cls, path: str, env, cfg: PPOConfig | None = None, seed: int = 0) -> "PPO":
+        """SB3 ``PPO.load(path, env)``: hyper-parameters from the zip's ``data`` (unless ``cfg``
+        is given), policy weights from its ``policy.pth``."""
+        sd, data = ckpt.load_sb3_zip(path)
+        if cfg is None:
+            fields = PPOConfig.__dataclass_fields__
+            cfg = PPOConfig(**{k: data[k] for k in fields if k in data})
+        model = cls(env, cfg, seed=seed)
+        model.policy.load_state_dict(sd)
+        model.loaded_num_timesteps = int(data.get("num_timesteps", 0))
+        return model

@@ -1,0 +1,130 @@
+"""CPU: SB3-layout checkpoint zips, the CheckpointCallback schedule and the newest-checkpoint
+rule of the reference (vectorized_env.py:124, visualize_policy.py:29-35).  Parity against SB3
+itself is unpinned (SB3 is not installed); the layout follows SB3 2.x save_to_zip_file."""
+import io
+import json
+import os
+import zipfile
+
+import pytest
+import torch
+
+
+@pytest.fixture(scope="module")
+def ck(pkg):
+    from importlib import import_module
+    return import_module(pkg.__name__ + ".checkpoint")
+
+
+@pytest.fixture(scope="module")
+def shapes(pkg):
+    from importlib import import_module
+    pol = import_module(pkg.__name__ + ".policy")
+    return [(k, pol._shape(s, 8)) for k, s in pol.PARAM_SPECS]
+
+
+def random_sd(shapes, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return {k: torch.randn(s, generator=g) for k, s in shapes}
+
+
+def test_zip_roundtrip_and_layout(ck, shapes, tmp_path):
+    sd = random_sd(shapes)
+    p = ck.save_sb3_zip(str(tmp_path / "m"), sd, num_timesteps=1234, data={"n_steps": 10})
+    assert p.endswith("m.zip") and os.path.exists(p)
+    with zipfile.ZipFile(p) as z:
+        names = set(z.namelist())
+        assert {"data", "policy.pth", "pytorch_variables.pth", "_stable_baselines3_version",
+                "system_info.txt"} <= names
+        data = json.loads(z.read("data"))
+        # policy.pth is a plain tensor dict: the safe loader reads it
+        sd2 = torch.load(io.BytesIO(z.read("policy.pth")), weights_only=True)
+    assert data["num_timesteps"] == 1234 and data["n_steps"] == 10
+    assert {"policy_class", "observation_space", "action_space"} <= set(data)
+    assert list(sd2) == list(sd)
+    sd3, data3 = ck.load_sb3_zip(p)
+    assert data3 == data
+    for k in sd:
+        assert torch.equal(sd3[k], sd[k])
+
+
+def test_zip_rejects_incomplete_state(ck, shapes, tmp_path):
+    sd = random_sd(shapes)
+    del sd["log_std"]
+    with pytest.raises(KeyError):
+        ck.save_sb3_zip(str(tmp_path / "bad.zip"), sd, num_timesteps=1)
+    with zipfile.ZipFile(tmp_path / "notmodel.zip", "w") as z:
+        z.writestr("data", "{}")
+    with pytest.raises(ValueError):
+        ck.load_sb3_zip(str(tmp_path / "notmodel.zip"))
+
+
+def test_optimizer_state_sliced_per_sb3_tensor(ck, shapes):
+    n = sum(torch.Size(s).numel() for _, s in shapes)
+    flat = torch.nn.Parameter(torch.zeros(n))
+    opt = torch.optim.Adam([flat], lr=1e-3, eps=1e-5)
+    flat.grad = torch.arange(n, dtype=torch.float32)
+    opt.step()
+    st = ck.optimizer_state_from_flat(shapes, opt.state_dict())
+    assert st["param_groups"][0]["params"] == list(range(13))
+    assert st["param_groups"][0]["eps"] == 1e-5
+    offs, o = {}, 0
+    for k, s in shapes:
+        offs[k] = o
+        o += torch.Size(s).numel()
+    for i, k in enumerate(ck.SB3_PARAM_ORDER):
+        s = dict(shapes)[k]
+        ea = st["state"][i]["exp_avg"]
+        assert tuple(ea.shape) == tuple(s)
+        exp = opt.state_dict()["state"][0]["exp_avg"][offs[k]:offs[k] + ea.numel()].reshape(s)
+        assert torch.equal(ea, exp)
+
+
+def test_latest_checkpoint_rule(ck, tmp_path):
+    for t in (20, 100, 3, 99):
+        (tmp_path / ck.checkpoint_name(t)).write_bytes(b"")
+    (tmp_path / "notes.txt").write_text("x")
+    assert ck.latest_checkpoint(str(tmp_path)).endswith("rl_model_100_steps.zip")
+    (tmp_path / "empty").mkdir()
+    with pytest.raises(FileNotFoundError):
+        ck.latest_checkpoint(str(tmp_path / "empty"))
+
+
+class FakeModel:
+    def __init__(self):
+        self.num_timesteps = 0
+        self.saves = []
+
+    def save(self, path, num_timesteps):
+        self.saves.append((os.path.basename(path), num_timesteps))
+
+
+@pytest.mark.parametrize("save_freq,n_steps", [(10, 10), (4, 10), (25, 10), (3, 1)])
+def test_callback_schedule_matches_sb3(ck, save_freq, n_steps, tmp_path):
+    """SB3: one _on_step per env step, save when n_calls % save_freq == 0, file named by the
+    num_timesteps at that step."""
+    A = 7
+    m = FakeModel()
+    cb = ck.CheckpointCallback(save_freq, str(tmp_path))
+    expect = []
+    calls = 0
+    for rollout in range(6):
+        for s in range(n_steps):
+            calls += 1
+            if calls % save_freq == 0:
+                expect.append(ck.checkpoint_name((rollout * n_steps + s + 1) * A))
+        m.num_timesteps += n_steps * A
+        cb.on_steps(m, n_steps, A)
+    assert [n for n, _ in m.saves] == expect
+    assert all(t == int(n.split("_")[-2]) for n, t in m.saves)
+    with pytest.raises(ValueError):
+        ck.CheckpointCallback(0, str(tmp_path))
+
+
+def test_train_cli_overrides(pkg):
+    from importlib import import_module
+    config = import_module(pkg.__name__ + ".config")
+    cfg = config.load_config(overrides=["name=run7", "num_agents_per_formation=7",
+                                        "+num_steps=30", "goal_in_obs=false"])
+    assert (cfg.name, cfg.num_agents_per_formation, cfg.num_steps, cfg.goal_in_obs) == \
+        ("run7", 7, 30, False)
