@@ -306,11 +306,20 @@ struct PolicyLane {
     float logp;   // sum over both components of Normal(mu, std).log_prob(act) (both halves)
 };
 
+// The Philox4x32-10 words (x, y) a row's Gaussian noise is made from (Box-Muller below):
+// counter (row, offset), key seed.  The oracle regenerates them (policy_oracle.philox_normals).
+__device__ __forceinline__ uint2 policy_noise_bits(int64_t row, uint64_t seed, uint64_t offset) {
+    const uint4 r = philox4x32(make_uint4((uint32_t)row, (uint32_t)((uint64_t)row >> 32),
+                                          (uint32_t)offset, (uint32_t)(offset >> 32)),
+                               (uint32_t)seed, (uint32_t)(seed >> 32));
+    return make_uint2(r.x, r.y);
+}
+
 // Full policy evaluation of one 32-agent tile.  bo = obs_operand(agent's observation row, h);
-// `row` is the agent's row in the batch (Philox counter); value_only skips the actor.
-__device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo, int lane, int64_t row, uint64_t seed,
-                                                  uint64_t offset, bool deterministic,
-                                                  bool value_only) {
+// nb = policy_noise_bits of the lane's agent (unused when deterministic); value_only skips the
+// actor.
+__device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo, int lane,
+                                                  uint2 nb, bool deterministic, bool value_only) {
     const int h = lane >> 5;
     PolicyLane o;
     f32x16 c0, c1;
@@ -334,11 +343,8 @@ __device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo
     o.mu = pa + lds[oSc + h];
     float a = o.mu;
     if (!deterministic) {
-        const uint4 r = philox4x32(make_uint4((uint32_t)row, (uint32_t)((uint64_t)row >> 32),
-                                              (uint32_t)offset, (uint32_t)(offset >> 32)),
-                                   (uint32_t)seed, (uint32_t)(seed >> 32));
-        const float u1 = (float)((r.x >> 8) + 1u) * 0x1.0p-24f;  // (0, 1]
-        const float u2 = (float)(r.y >> 8) * 0x1.0p-24f;          // [0, 1)
+        const float u1 = (float)((nb.x >> 8) + 1u) * 0x1.0p-24f;  // (0, 1]
+        const float u2 = (float)(nb.y >> 8) * 0x1.0p-24f;          // [0, 1)
         // Box-Muller on the hardware transcendentals: v_log_f32 is log2, v_sin/v_cos_f32 take
         // the angle in turns (sin(2 pi u2) directly, no range reduction needed for u2 in [0,1))
         const float rad = __builtin_amdgcn_sqrtf(-1.38629436111989061f * __builtin_amdgcn_logf(u1));

@@ -36,8 +36,9 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
         float o[8];
 #pragma unroll
         for (int col = 0; col < 8; ++col) o[col] = (valid && col < D) ? obs[row * D + col] : 0.0f;
-        const PolicyLane r = policy_tile(lds, obs_operand(o, h), lane, row, seed, offset,
-                                         deterministic != 0, value_only);
+        const uint2 nb = deterministic ? make_uint2(0u, 0u) : policy_noise_bits(row, seed, offset);
+        const PolicyLane r = policy_tile(lds, obs_operand(o, h), lane, nb, deterministic != 0,
+                                         value_only);
         if (valid) {
             if (mu_out) mu_out[row * 2 + h] = r.mu;
             if (act_out) act_out[row * 2 + h] = r.act;

@@ -49,20 +49,6 @@ constexpr int kPRWaves = FENV_PR_WAVES;
 constexpr size_t kPRLdsBytes = (size_t)(kPolicyLds + kPRWaves * 512) * sizeof(float);
 static_assert(kPolicyLds % 4 == 0, "stage slices must stay 16-byte aligned");
 
-// Copy nf floats from a wave's LDS slice to global memory with the widest aligned stores.
-__device__ __forceinline__ void store_span(const float *stage, int nf, float *dst, int lane) {
-    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
-    if ((ad & 15) == 0 && (nf & 3) == 0) {
-        for (int q = lane; q < (nf >> 2); q += 64)
-            reinterpret_cast<float4 *>(dst)[q] = reinterpret_cast<const float4 *>(stage)[q];
-    } else if ((ad & 7) == 0 && (nf & 1) == 0) {
-        for (int q = lane; q < (nf >> 1); q += 64)
-            reinterpret_cast<float2 *>(dst)[q] = reinterpret_cast<const float2 *>(stage)[q];
-    } else {
-        for (int q = lane; q < nf; q += 64) dst[q] = stage[q];
-    }
-}
-
 // The layer-1 MFMA B operands of the wave's two tiles from the staged observation rows.
 template <int D>
 __device__ __forceinline__ void tile_operands(const float *stage, int j, int h, h8 (&bo)[2]) {
@@ -137,13 +123,18 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         h8 bo[2];
         tile_operands<D>(stage, j, h, bo);
         __builtin_amdgcn_wave_barrier();
+        // Gaussian noise words: lane (j, h) draws them for agent j of tile h, so one Philox call
+        // per lane covers both tiles (each agent keeps its own (row, step) counter)
+        const uint2 mine = det ? make_uint2(0u, 0u)
+                               : policy_noise_bits(a_first + 32 * h + j, g.seed, g.offset + k);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            // one tile at a time, outputs parked in LDS at once (keeps the step under 128 VGPRs)
+            // one tile at a time, outputs parked in LDS at once
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            const PolicyLane pl = policy_tile(wimg, bo[t], ln, a_first + 32 * t + j, g.seed,
-                                              g.offset + k, det, false);
+            uint2 nb = mine;
+            if (!det) nb = make_uint2(__shfl(mine.x, j + 32 * t, 64), __shfl(mine.y, j + 32 * t, 64));
+            const PolicyLane pl = policy_tile(wimg, bo[t], ln, nb, det, false);
             const int r = 32 * t + j;
             stage[2 * r + h] = pl.mu;
             stage[128 + 2 * r + h] = pl.act;
@@ -154,12 +145,18 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (b.mu) store_span(stage, 2 * M, b.mu + (rk + a_first) * 2, ln);
-        store_span(stage + 128, 2 * M, b.action + (rk + a_first) * 2, ln);
-        if (b.clipped) store_span(stage + 256, 2 * M, b.clipped + (rk + a_first) * 2, ln);
-        store_span(stage + 384, M, b.value + rk + a_first, ln);
-        store_span(stage + 448, M, b.log_prob + rk + a_first, ln);
-        const float2 ac = reinterpret_cast<const float2 *>(stage + 256)[ln];
+        // one store per output: lane l writes agent a_first + l (bases are wave-uniform, so the
+        // per-lane part of every address is a 32-bit offset)
+        const int64_t o1 = rk + a_first;
+        const float2 *s2 = reinterpret_cast<const float2 *>(stage);
+        if (ln < M) {
+            if (b.mu) reinterpret_cast<float2 *>(b.mu + 2 * o1)[ln] = s2[ln];
+            reinterpret_cast<float2 *>(b.action + 2 * o1)[ln] = s2[64 + ln];
+            if (b.clipped) reinterpret_cast<float2 *>(b.clipped + 2 * o1)[ln] = s2[128 + ln];
+            (b.value + o1)[ln] = stage[384 + ln];
+            (b.log_prob + o1)[ln] = stage[448 + ln];
+        }
+        const float2 ac = s2[128 + ln];
         __builtin_amdgcn_wave_barrier();
 
         // env.step(clipped actions) (collect_rollouts clips to the Box, vectorized_env.py:68-82)
@@ -167,10 +164,10 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         bool dn, rs;
         env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
         any_reset |= rs;
-        if (active) {
-            b.reward[rk + a] = rw;
-            b.episode_start[rk + a] = (uint8_t)start;
-            if (b.done) b.done[rk + a] = (uint8_t)dn;
+        if (active) {  // active <=> ln < M; agent a = a_first + ln
+            (b.reward + o1)[ln] = rw;
+            (b.episode_start + o1)[ln] = (uint8_t)start;
+            if (b.done) (b.done + o1)[ln] = (uint8_t)dn;
         }
         start = dn ? 1u : 0u;
         env_obs<D>(x, s, o);
@@ -193,7 +190,7 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         for (int t = 0; t < 2; ++t) {
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            const PolicyLane pv = policy_tile(wimg, bo[t], lane, 0, 0, 0, true, true);
+            const PolicyLane pv = policy_tile(wimg, bo[t], lane, make_uint2(0u, 0u), true, true);
             if (h == 0) stage[384 + 32 * t + j] = pv.value;
         }
         __builtin_amdgcn_wave_barrier();
