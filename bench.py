@@ -111,6 +111,39 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
             "bound": "VALU issue (256 exp+rcp tanh per agent-step), see DESIGN.md"}
 
 
+def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: int = 50,
+                     T: int = 10) -> dict:
+    """Secondary env-only lines (BASELINE configs 2 and 5): fused T-step rollouts of the given
+    shape with HBM-resident actions, avg launch time from HIP events on the launch stream."""
+    import torch
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode="philox")
+    A = env.num_envs
+    acts = torch.rand((T, A, 2), device=dev) * 2 - 1
+    obs = torch.empty((T, A, 8), device=dev)
+    rew = torch.empty((T, A), device=dev)
+    done = torch.empty((T, A), dtype=torch.bool, device=dev)
+    env.reset_tensor()
+    for _ in range(3):
+        env.rollout(acts, obs, rew, done)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for _ in range(launches):
+        env.rollout(acts, obs, rew, done)
+    b.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = a.elapsed_time(b) / launches
+    byts = rollout_bytes_per_launch(A, agents, 8, T)
+    return {"workload": f"{formations} formations x {agents} agents, fused {T}-step rollouts",
+            "value": A * T * launches / el, "unit": "agent-steps/s", "avg_kernel_ms": ms,
+            "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def load_pmc_traffic(workload: str):
     """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -145,6 +178,8 @@ def main():
     ap.add_argument("--stats-every", type=int, default=10,
                     help="reduce + all-reduce the episode stats every this many rollouts")
     ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the secondary env-only lines (BASELINE configs 2 and 5)")
     args = ap.parse_args()
 
     import torch
@@ -273,6 +308,9 @@ def main():
                                     "every_rollouts": args.stats_every}
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
+        if world == 1 and not args.no_configs:
+            out["env_configs"] = {"config2": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
+                                  "config5": env_config_bench(pkg.__name__, dev, 16384, 64)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
