@@ -113,7 +113,7 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
 
 def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: int = 50,
                      T: int = 10) -> dict:
-    """Secondary env-only lines (BASELINE configs 2 and 5): fused T-step rollouts of the given
+    """Secondary env-only lines (BASELINE.json configs[1] and [4]): fused T-step rollouts of the given
     shape with HBM-resident actions, avg launch time from HIP events on the launch stream."""
     import torch
     from importlib import import_module
@@ -179,7 +179,7 @@ def main():
                     help="reduce + all-reduce the episode stats every this many rollouts")
     ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the secondary env-only lines (BASELINE configs 2 and 5)")
+                    help="skip the secondary env-only lines (BASELINE configs[1] and [4])")
     args = ap.parse_args()
 
     import torch
@@ -309,8 +309,8 @@ def main():
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
         if world == 1 and not args.no_configs:
-            out["env_configs"] = {"config2": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
-                                  "config5": env_config_bench(pkg.__name__, dev, 16384, 64)}
+            out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
+                                  "config4": env_config_bench(pkg.__name__, dev, 16384, 64)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
