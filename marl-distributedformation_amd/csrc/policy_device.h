@@ -49,6 +49,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef FENV_SPLIT_MIX
+#define FENV_SPLIT_MIX 1
+#endif
 #ifndef FENV_POLICY_PRIO
 #define FENV_POLICY_PRIO 0
 #endif
@@ -117,9 +120,21 @@ __device__ __forceinline__ void split8(const V &v, int base, h8 &hi, h8 &lo) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const float x = v[base + 2 * p], y = v[base + 2 * p + 1];
+#if FENV_SPLIT_MIX
+        // hi = RTZ to f16 (the 11 leading significant bits); the exact remainder x - f32(hi)
+        // straight from the packed halves with v_fma_mix_f32 (f16 operand, f32 math)
+        const uint32_t hh = pk_rtz(x, y);
+        float lx, ly;
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lx) : "v"(hh), "v"(x));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "=v"(ly) : "v"(hh), "v"(y));
+        H[p] = hh;
+        L[p] = pk_rtz(lx, ly);
+#else
         const float xh = hi11(x), yh = hi11(y);
         H[p] = pk_rtz(xh, yh);
         L[p] = pk_rtz(x - xh, y - yh);
+#endif
     }
     hi = __builtin_bit_cast(h8, H);
     lo = __builtin_bit_cast(h8, L);
