@@ -71,7 +71,8 @@ def evaluate_actions(policy: MlpPolicy, flat: torch.Tensor, obs: torch.Tensor,
 class PPO:
     """Minimal on-device PPO: collect (HIP kernels) -> GAE (HIP) -> clipped-surrogate update."""
 
-    def __init__(self, env, cfg: PPOConfig | None = None, seed: int = 0, policy=None):
+    def __init__(self, env, cfg: PPOConfig | None = None, seed: int = 0, policy=None,
+                 use_graph: bool | None = None):
         self.cfg = cfg or PPOConfig()
         self.seed = int(seed)
         self.env = env
@@ -80,46 +81,136 @@ class PPO:
                                     self.cfg.gamma, self.cfg.gae_lambda)
         self.collector = RolloutCollector(env, self.policy, self.buffer, seed=seed)
         self.param = torch.nn.Parameter(self.policy.flat)  # shares storage with the kernel's
-        self.opt = torch.optim.Adam([self.param], lr=self.cfg.learning_rate, eps=1e-5)
+        self.param.grad = torch.zeros_like(self.param)     # static: graph replays write it
+        # capturable: the step count lives on the device, so the update can be graph-captured
+        self.opt = torch.optim.Adam([self.param], lr=self.cfg.learning_rate, eps=1e-5,
+                                    capturable=True)
         self.gen = torch.Generator(device=env.device).manual_seed(seed)
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.stats: dict = {}
+        # minibatch update as HIP graphs (one replay per minibatch instead of ~60 launches)
+        self.use_graph = (self.param.device.type == "cuda") if use_graph is None else use_graph
+        n = self.buffer.n_steps * self.buffer.n_envs
+        dev = self.param.device
+        self._perm = torch.zeros(n, dtype=torch.long, device=dev)
+        self._k = torch.zeros((), dtype=torch.long, device=dev)
+        self._sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        self._graphs = None
 
     @property
     def num_timesteps(self) -> int:
         return self.collector.num_timesteps * self.world
 
-    def train(self) -> dict:
+    # ---------------------------------------------------------------- one minibatch
+    def _flat(self):
+        b, n = self.buffer, self.buffer.n_steps * self.buffer.n_envs
+        return (b.observations.reshape(n, b.obs_dim), b.actions.reshape(n, 2),
+                b.log_probs.reshape(n), b.advantages.reshape(n), b.returns.reshape(n))
+
+    def _forward_backward(self, idx: torch.Tensor) -> None:
+        """SB3 PPO.train inner loop up to loss.backward() for minibatch ``idx``; adds the
+        minibatch's (policy loss, value loss, entropy loss, clip fraction) to self._sums."""
         c = self.cfg
-        pg, vl, el, cf, n = 0.0, 0.0, 0.0, 0.0, 0
+        obs, act, old_lp, adv, ret = (t[idx] for t in self._flat())
+        values, log_prob, entropy = evaluate_actions(self.policy, self.param, obs, act)
+        if c.normalize_advantage and adv.numel() > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(log_prob - old_lp)
+        l1 = adv * ratio
+        l2 = adv * torch.clamp(ratio, 1 - c.clip_range, 1 + c.clip_range)
+        policy_loss = -torch.min(l1, l2).mean()
+        value_loss = Fn.mse_loss(ret, values)
+        entropy_loss = -torch.mean(entropy)
+        loss = policy_loss + c.ent_coef * entropy_loss + c.vf_coef * value_loss
+        self.param.grad.zero_()
+        loss.backward()
+        clip_fraction = (torch.abs(ratio - 1) > c.clip_range).float().mean()
+        self._sums += torch.stack([policy_loss.detach(), value_loss.detach(),
+                                   entropy_loss.detach(), clip_fraction]).double()
+
+    def _apply(self) -> None:
+        torch.nn.utils.clip_grad_norm_([self.param], self.cfg.max_grad_norm)
+        self.opt.step()
+
+    def _allreduce(self) -> None:
+        if self.world > 1:  # one flat 9,669-float bucket per optimizer step (RCCL)
+            dist.all_reduce(self.param.grad)
+            self.param.grad.div_(self.world)
+
+    def _eager_step(self, idx: torch.Tensor) -> None:
+        self._forward_backward(idx)
+        self._allreduce()
+        self._apply()
+
+    def _capture(self, warm_idx: list) -> None:
+        """Record the full-minibatch step as HIP graph(s): [gather + forward + backward +
+        stats, k += 1] and [clip + Adam] (one graph when there is no all-reduce between).
+        The warm-up runs the first real minibatches eagerly on the capture stream."""
+        bs = self.cfg.batch_size
+        # every tensor the graphs read must outlive them (a freed one's memory gets reused and
+        # the replay would gather with garbage indices): attributes, not locals
+        self._ar = torch.arange(bs, device=self.param.device)
+        ar = self._ar
+        s = torch.cuda.Stream(self.param.device)
+        s.wait_stream(torch.cuda.current_stream(self.param.device))
+        with torch.cuda.stream(s):
+            for idx in warm_idx:
+                self._eager_step(idx)
+
+            def fb():
+                self._forward_backward(self._perm[self._k * bs + ar])
+                self._k += 1
+
+            g1 = torch.cuda.CUDAGraph()
+            if self.world > 1:
+                with torch.cuda.graph(g1, stream=s):
+                    fb()
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2, stream=s):
+                    self._apply()
+                self._graphs = (g1, g2)
+            else:
+                with torch.cuda.graph(g1, stream=s):
+                    fb()
+                    self._apply()
+                self._graphs = (g1, None)
+        torch.cuda.current_stream(self.param.device).wait_stream(s)
+
+    def train(self) -> dict:
+        """SB3 ``PPO.train``: n_epochs over shuffled minibatches of the rollout buffer (the same
+        randperm per epoch as ``RolloutBuffer.get``).  Full minibatches replay the captured
+        graph(s); a trailing partial minibatch runs eagerly.  Losses are summed on the device and
+        read once at the end."""
+        c = self.cfg
+        n = self.buffer.n_steps * self.buffer.n_envs
+        bs = min(int(c.batch_size), n)
+        nfull, rem = divmod(n, bs)
+        self._sums.zero_()
+        steps = 0
+        graph = self.use_graph and bs == c.batch_size and nfull > 0
         for _ in range(c.n_epochs):
-            for b in self.buffer.get(c.batch_size, self.gen):
-                values, log_prob, entropy = evaluate_actions(self.policy, self.param,
-                                                             b.observations, b.actions)
-                adv = b.advantages
-                if c.normalize_advantage and adv.numel() > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                ratio = torch.exp(log_prob - b.old_log_prob)
-                l1 = adv * ratio
-                l2 = adv * torch.clamp(ratio, 1 - c.clip_range, 1 + c.clip_range)
-                policy_loss = -torch.min(l1, l2).mean()
-                value_loss = Fn.mse_loss(b.returns, values)
-                entropy_loss = -torch.mean(entropy)
-                loss = policy_loss + c.ent_coef * entropy_loss + c.vf_coef * value_loss
-                self.opt.zero_grad(set_to_none=False)
-                loss.backward()
-                if self.world > 1:  # one flat bucket per optimizer step
-                    dist.all_reduce(self.param.grad)
-                    self.param.grad.div_(self.world)
-                torch.nn.utils.clip_grad_norm_([self.param], c.max_grad_norm)
-                self.opt.step()
-                pg += float(policy_loss.detach())
-                vl += float(value_loss.detach())
-                el += float(entropy_loss.detach())
-                cf += float((torch.abs(ratio - 1) > c.clip_range).float().mean())
-                n += 1
-        self.stats = dict(policy_gradient_loss=pg / n, value_loss=vl / n, entropy_loss=el / n,
-                          clip_fraction=cf / n)
+            self._perm.copy_(torch.randperm(n, device=self.param.device, generator=self.gen))
+            self._k.zero_()
+            first = 0
+            if graph and self._graphs is None:
+                warm = min(3, nfull)
+                self._capture([self._perm[i * bs:(i + 1) * bs] for i in range(warm)])
+                first = warm
+                self._k.fill_(warm)
+            for i in range(first, nfull):
+                if graph:
+                    self._graphs[0].replay()
+                    if self._graphs[1] is not None:
+                        self._allreduce()
+                        self._graphs[1].replay()
+                else:
+                    self._eager_step(self._perm[i * bs:(i + 1) * bs])
+            if rem:
+                self._eager_step(self._perm[nfull * bs:])
+            steps += nfull + (1 if rem else 0)
+        m = (self._sums / steps).tolist()
+        self.stats = dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2],
+                          clip_fraction=m[3])
         return self.stats
 
     def learn(self, total_timesteps: int, callback=None) -> "PPO":
