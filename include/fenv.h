@@ -178,6 +178,27 @@ int fenv_policy_rollout(fenv_t *env, const float *params, int32_t T, uint64_t se
                         uint64_t offset, int32_t deterministic, float gamma, float gae_lambda,
                         const fenv_rollout_bufs *bufs, void *stream);
 
+/* ------------------------------------------------------------------ PPO update
+ * SB3 2.x PPO.train for small minibatches (batch_size <= 64, the SB3 default under
+ * vectorized_env.py:126-131) in ONE single-workgroup launch: for each of n_epochs, the n
+ * samples in the order perm[epoch][0..n) split into minibatches of batch_size (the last one
+ * partial); per minibatch the clipped surrogate + vf_coef * MSE(returns, values) + ent_coef *
+ * entropy loss (advantages normalised per minibatch when normalize_advantage), backward,
+ * clip_grad_norm_(max_grad_norm), Adam (torch semantics, bias-corrected).  params [P] (the
+ * policy_forward layout) are updated in place; exp_avg / exp_avg_sq [P] and *step (one float)
+ * are the Adam state (device); stats (device, 4 doubles) are INCREMENTED by the per-minibatch
+ * policy loss, value loss, entropy loss and clip fraction.  Sample buffers (device): obs [n][D],
+ * actions [n][2] (unclipped), old_log_prob, advantages, returns [n]; perm int64 [n_epochs][n]. */
+typedef struct ppo_hparams {
+    float clip_range, ent_coef, vf_coef, max_grad_norm, lr, beta1, beta2, eps;
+    int32_t normalize_advantage;
+} ppo_hparams;
+int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
+               const float *obs, const float *actions, const float *old_log_prob,
+               const float *advantages, const float *returns, int64_t n, const int64_t *perm,
+               int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
+               void *stream);
+
 const char *fenv_last_error(void);
 
 #ifdef __cplusplus

@@ -52,8 +52,17 @@ SIGNATURES = {
                            _P]),
     "fenv_policy_rollout": (_I32, [_P, _P, _I32, _U64, _U64, _I32, ctypes.c_float,
                                    ctypes.c_float, _P, _P]),
+    "ppo_update": (_I32, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P, _I32, _I32, _P,
+                          _P, _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
+
+
+class PPOHParams(ctypes.Structure):
+    """``ppo_hparams`` (include/fenv.h)."""
+    _fields_ = [(k, ctypes.c_float) for k in ("clip_range", "ent_coef", "vf_coef",
+                                              "max_grad_norm", "lr", "beta1", "beta2", "eps")] + \
+        [("normalize_advantage", ctypes.c_int32)]
 
 
 class RolloutBufs(ctypes.Structure):

@@ -441,4 +441,22 @@ int rollout_gae(const float *rew, const float *values, const uint8_t *episode_st
     return FENV_OK;
 }
 
+int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
+               const float *obs, const float *actions, const float *old_log_prob,
+               const float *advantages, const float *returns, int64_t n, const int64_t *perm,
+               int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
+               void *stream) {
+    if (!params || !exp_avg || !exp_avg_sq || !step || !obs || !actions || !old_log_prob ||
+        !advantages || !returns || !perm || !hp || !stats)
+        return fail(FENV_EINVAL, "ppo_update: NULL argument");
+    if (obs_dim != 6 && obs_dim != 8) return fail(FENV_EINVAL, "ppo_update: obs_dim must be 6 or 8");
+    if (n < 1 || n_epochs < 0 || batch_size < 1 || batch_size > 64)
+        return fail(FENV_EINVAL, "ppo_update: need n >= 1 and 1 <= batch_size <= 64");
+    if (n_epochs == 0) return FENV_OK;
+    FENV_HIP(fenvk::launch_ppo_update(params, exp_avg, exp_avg_sq, step, obs_dim, obs, actions,
+                                      old_log_prob, advantages, returns, n, perm, n_epochs,
+                                      batch_size, *hp, stats, as_stream(stream)));
+    return FENV_OK;
+}
+
 }  // extern "C"

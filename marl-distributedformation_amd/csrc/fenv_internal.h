@@ -73,4 +73,11 @@ hipError_t launch_gae(const float *rew, const float *values, const uint8_t *epis
                       const float *last_values, const uint8_t *last_dones, int32_t T, int64_t A,
                       float gamma, float lam, float *adv, float *ret, hipStream_t st);
 
+hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
+                             int32_t D, const float *obs, const float *act,
+                             const float *old_log_prob, const float *adv, const float *ret,
+                             int64_t n, const int64_t *perm, int32_t n_epochs,
+                             int32_t batch_size, const ppo_hparams &hp, double *stats,
+                             hipStream_t st);
+
 }  // namespace fenvk

@@ -1,0 +1,382 @@
+// On-device PPO update (SB3 2.x PPO.train) for small minibatches, one workgroup-resident launch.
+//
+// Reference: PPO('MlpPolicy', env, n_steps=10, learning_rate=1e-3, ent_coef=0.01) with SB3
+// defaults (/root/reference/vectorized_env.py:126-131): n_epochs passes over the rollout buffer in
+// shuffled minibatches of batch_size = 64; per minibatch the clipped surrogate + vf_coef * value
+// loss + ent_coef * entropy loss, backward, clip_grad_norm_(0.5), Adam(eps 1e-5).  The torch
+// restatement of the same update is ppo.py (graph / eager paths); this kernel is its fused form.
+//
+// Why one workgroup: a minibatch step depends on the previous step's parameters, and a 64-sample
+// step of this 9,669-parameter MLP is ~1.8 MFLOP -- far too little to spread over the chip, and
+// ~100 tiny launches per step in torch (~430 us replayed as a HIP graph).  Here the parameters,
+// their gradients and the minibatch's activations live in LDS (151 KB), the Adam moments stay in
+// (L2-resident) global memory, and the loop runs every minibatch of every epoch inside one
+// launch.  The three 64-deep contractions are register-blocked 8 ways so a multiply-add costs
+// ~1 LDS read instead of 2.  All arithmetic is fp32 VALU (fmaf chains); results match the torch
+// path to summation-order rounding (tests/test_gpu_rollout.py).
+//
+// Work split per minibatch (B <= 64 samples, 16 waves, lane = sample or = hidden unit):
+//   forward  layer 1/2: wave w computes hidden units 8w..8w+7 (of 2 x 64) for lane = sample;
+//            activation rows are padded to 65 floats so the 64 lanes hit 64 banks.
+//   loss     wave 0, lane = sample: heads, log-prob, ratio, clipped surrogate, value loss, and the
+//            per-sample gradients w.r.t. mu, value, log_std (torch's min/clamp subgradients).
+//   backward head weights (lane = k), dL/dz2 in place of the layer-2 activations, W2/b2 grads
+//            (lane = k, wave-uniform row), dL/dz1 in place of layer 1, W1/b1 grads.
+//   update   global grad 2-norm (block reduction), clip, Adam with bias correction.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include "fenv.h"
+#include "fenv_internal.h"
+#include "policy_device.h"
+
+namespace fenvk {
+
+constexpr int kPB = 64;                         // max samples per minibatch
+constexpr int kPT = 512;                        // threads (8 waves; 256-VGPR budget)
+constexpr int kNW = kPT / 64;                   // waves
+constexpr int kRow = kHid + 1;                  // padded activation row
+constexpr int kMaxP = 9680;                     // >= policy_param_count(8) = 9,669
+constexpr int kPerT = (kMaxP + kPT - 1) / kPT;  // parameters owned per thread (Adam moments)
+
+// LDS layout (floats)
+constexpr int oPW = 0;                        // [kMaxP] parameters
+constexpr int oPG = oPW + kMaxP;              // [kMaxP] gradients
+constexpr int oPO = oPG + kMaxP;              // [kPB][9] observations (zero-padded to 8)
+constexpr int oPH1 = oPO + kPB * 9;           // [2][kPB][kRow] layer-1 tanh, then dL/dz1
+constexpr int oPH2 = oPH1 + 2 * kPB * kRow;   // [2][kPB][kRow] layer-2 tanh, then dL/dz2
+constexpr int oPS = oPH2 + 2 * kPB * kRow;    // [16][kPB] per-sample scalars
+constexpr int oPR = oPS + 16 * kPB;           // [64] reduction scratch
+constexpr int kPPOLds = oPR + 64;
+constexpr size_t kPPOLdsBytes = (size_t)kPPOLds * sizeof(float);
+
+// per-sample scalar slots
+enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV };
+
+struct PPOArgs {
+    float *params, *exp_avg, *exp_avg_sq, *step;
+    const float *obs, *act, *old_log_prob, *adv, *ret;
+    const int64_t *perm;
+    int64_t n;
+    int32_t D, n_epochs, batch_size;
+    ppo_hparams hp;
+    double *stats;
+};
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *W = sm + oPW, *G = sm + oPG, *O = sm + oPO, *H1 = sm + oPH1, *H2 = sm + oPH2;
+    float *S = sm + oPS, *R = sm + oPR;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int D = g.D;
+    const PLayout L(D);
+    const int P = L.total;
+    const ppo_hparams hp = g.hp;
+
+    for (int p = tid; p < P; p += kPT) W[p] = g.params[p];
+    float *__restrict__ m = g.exp_avg;  // Adam moments stay in global memory (L2-resident)
+    float *__restrict__ v = g.exp_avg_sq;
+    float step = g.step[0];
+    double st_pl = 0.0, st_vl = 0.0, st_el = 0.0, st_cf = 0.0;
+    __syncthreads();
+
+    const int64_t n = g.n;
+    const int bs = g.batch_size;
+    for (int ep = 0; ep < g.n_epochs; ++ep) {
+        const int64_t *perm = g.perm + (int64_t)ep * n;
+        for (int64_t s0 = 0; s0 < n; s0 += bs) {
+            const int B = (int)((n - s0) < bs ? (n - s0) : bs);
+            const float invB = 1.0f / (float)B;
+            // ---- gather the minibatch
+            for (int q = tid; q < B * 8; q += kPT) {
+                const int b = q >> 3, i = q & 7;
+                const int64_t r = perm[s0 + b];
+                O[b * 9 + i] = i < D ? g.obs[r * D + i] : 0.0f;
+            }
+            for (int b = tid; b < B; b += kPT) {
+                const int64_t r = perm[s0 + b];
+                S[sA0 * kPB + b] = g.act[2 * r];
+                S[sA1 * kPB + b] = g.act[2 * r + 1];
+                S[sOLP * kPB + b] = g.old_log_prob[r];
+                S[sADV * kPB + b] = g.adv[r];
+                S[sRET * kPB + b] = g.ret[r];
+            }
+            __syncthreads();
+            // ---- advantage normalisation (wave 0) || layer 1 (all waves)
+            if (w == 0 && hp.normalize_advantage && B > 1) {
+                const float a = lane < B ? S[sADV * kPB + lane] : 0.0f;
+                const float mean = wsum(a) * invB;
+                const float d = lane < B ? a - mean : 0.0f;
+                const float sd = __builtin_sqrtf(wsum(d * d) / (float)(B - 1));
+                if (lane < B) S[sADV * kPB + lane] = (a - mean) / (sd + 1e-8f);
+            }
+            if (lane < B) {
+                for (int u = w; u < 2 * kHid; u += kNW) {
+                    const int net = u >> 6, j = u & 63;
+                    const float *w1 = W + (net ? L.vf0W : L.pi0W) + j * D;
+                    float z = W[(net ? L.vf0b : L.pi0b) + j];
+                    for (int i = 0; i < D; ++i) z = __builtin_fmaf(w1[i], O[lane * 9 + i], z);
+                    H1[(net * kPB + lane) * kRow + j] = tanhf(z);
+                }
+            }
+            __syncthreads();
+            // ---- layer 2: lane = sample, 8 units per wave; per 4 k one h read per k and one
+            // broadcast ds_read_b128 of W2 per unit (the fmaf chain over k keeps its order)
+            for (int grp = w; grp < 16 && lane < B; grp += kNW) {
+                const int net = (8 * grp) >> 6, j0 = (8 * grp) & 63;
+                const float *w2 = W + (net ? L.vf2W : L.pi2W) + j0 * kHid;
+                const float *h = H1 + (net * kPB + lane) * kRow;
+                float acc[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc[u] = W[(net ? L.vf2b : L.pi2b) + j0 + u];
+#pragma unroll 1
+                for (int k = 0; k < kHid; k += 4) {
+                    const float h0 = h[k], h1 = h[k + 1], h2 = h[k + 2], h3 = h[k + 3];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const f32x4 wv = *reinterpret_cast<const f32x4 *>(w2 + u * kHid + k);
+                        acc[u] = __builtin_fmaf(wv[0], h0, acc[u]);
+                        acc[u] = __builtin_fmaf(wv[1], h1, acc[u]);
+                        acc[u] = __builtin_fmaf(wv[2], h2, acc[u]);
+                        acc[u] = __builtin_fmaf(wv[3], h3, acc[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) H2[(net * kPB + lane) * kRow + j0 + u] = tanhf(acc[u]);
+            }
+            __syncthreads();
+            // ---- heads, losses and per-sample gradients (wave 0, lane = sample)
+            if (w == 0) {
+                const bool on = lane < B;
+                const float ls0 = W[L.logstd], ls1 = W[L.logstd + 1];
+                const float sd0 = expf(ls0), sd1 = expf(ls1);
+                const float var0 = sd0 * sd0, var1 = sd1 * sd1;
+                const float lsd0 = logf(sd0), lsd1 = logf(sd1);  // torch: std.log()
+                float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
+                float gv = 0.f;
+                if (on) {
+                    const float *ha = H2 + lane * kRow, *hv = H2 + (kPB + lane) * kRow;
+                    float mu0 = 0.f, mu1 = 0.f, val = 0.f;
+                    for (int k = 0; k < kHid; ++k) {
+                        mu0 = __builtin_fmaf(W[L.actW + k], ha[k], mu0);
+                        mu1 = __builtin_fmaf(W[L.actW + kHid + k], ha[k], mu1);
+                        val = __builtin_fmaf(W[L.valW + k], hv[k], val);
+                    }
+                    mu0 += W[L.actb];
+                    mu1 += W[L.actb + 1];
+                    val += W[L.valb];
+                    const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
+                    const float d0 = a0 - mu0, d1 = a1 - mu1;
+                    const float kLogSqrt2Pi = 0.918938533204672742f;
+                    const float lp = (-(d0 * d0) / (2.0f * var0) - lsd0 - kLogSqrt2Pi) +
+                                     (-(d1 * d1) / (2.0f * var1) - lsd1 - kLogSqrt2Pi);
+                    const float ratio = expf(lp - S[sOLP * kPB + lane]);
+                    const float an = S[sADV * kPB + lane];
+                    const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
+                    const float rc = ratio < lo ? lo : (ratio > hi ? hi : ratio);
+                    const float l1 = an * ratio, l2 = an * rc;
+                    pl = l1 < l2 ? l1 : l2;
+                    cf = fabsf(ratio - 1.0f) > hp.clip_range ? 1.0f : 0.0f;
+                    const float rr = S[sRET * kPB + lane] - val;
+                    vl = rr * rr;
+                    // torch.minimum: ties split the gradient; clamp passes it inside [lo, hi]
+                    const float g1 = l1 < l2 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f);
+                    const float g2 = l2 < l1 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f);
+                    const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+                    const float dratio = -(g1 * an + g2 * an * inside) * invB;
+                    const float dlp = dratio * ratio;
+                    gv = hp.vf_coef * (-2.0f * rr) * invB;
+                    gmu0 = dlp * d0 / var0;
+                    gmu1 = dlp * d1 / var1;
+                    gls0 = dlp * (d0 * d0 / var0 - 1.0f);
+                    gls1 = dlp * (d1 * d1 / var1 - 1.0f);
+                }
+                S[sGMU0 * kPB + lane] = gmu0;
+                S[sGMU1 * kPB + lane] = gmu1;
+                S[sGV * kPB + lane] = gv;
+                pl = wsum(pl);
+                vl = wsum(vl);
+                cf = wsum(cf);
+                gls0 = wsum(gls0);
+                gls1 = wsum(gls1);
+                const float sgmu0 = wsum(gmu0), sgmu1 = wsum(gmu1), sgv = wsum(gv);
+                if (lane == 0) {
+                    const float kHalfLog2PiE = 1.41893853320467274f;  // 0.5 + 0.5 log(2 pi)
+                    const float ent = (kHalfLog2PiE + lsd0) + (kHalfLog2PiE + lsd1);
+                    st_pl += (double)(-pl * invB);
+                    st_vl += (double)(vl * invB);
+                    st_el += (double)(-ent);
+                    st_cf += (double)(cf * invB);
+                    // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls = 1)
+                    G[L.logstd] = gls0 - hp.ent_coef;
+                    G[L.logstd + 1] = gls1 - hp.ent_coef;
+                    G[L.actb] = sgmu0;
+                    G[L.actb + 1] = sgmu1;
+                    G[L.valb] = sgv;
+                }
+            }
+            __syncthreads();
+            // ---- head weight gradients (waves 0-2, lane = hidden unit k)
+            if (w < 3) {
+                const int slot = w == 0 ? sGMU0 : (w == 1 ? sGMU1 : sGV);
+                const float *h = H2 + (w == 2 ? kPB : 0) * kRow;
+                float acc = 0.f;
+                for (int b = 0; b < B; ++b) acc = __builtin_fmaf(S[slot * kPB + b], h[b * kRow + lane], acc);
+                G[(w == 2 ? L.valW : L.actW + w * kHid) + lane] = acc;
+            }
+            __syncthreads();
+            // ---- dL/dz2 in place (pairs (net, b): wave w handles 8 of them, lane = k)
+            for (int pr = w; pr < 2 * kPB; pr += kNW) {
+                const int net = pr >> 6, b = pr & 63;
+                if (b < B) {
+                    float *hp2 = H2 + (net * kPB + b) * kRow + lane;
+                    const float gh = net ? S[sGV * kPB + b] * W[L.valW + lane]
+                                         : S[sGMU0 * kPB + b] * W[L.actW + lane] +
+                                               S[sGMU1 * kPB + b] * W[L.actW + kHid + lane];
+                    const float h = *hp2;
+                    *hp2 = gh * (1.0f - h * h);
+                }
+            }
+            __syncthreads();
+            // ---- W2 gradients (rows (net, j0..j0+7) per wave, lane = k): one h1 read and 8
+            // broadcast dL/dz2 reads per sample
+            for (int grp = w; grp < 16; grp += kNW) {
+                const int net = (8 * grp) >> 6, j0 = (8 * grp) & 63;
+                float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+                for (int b = 0; b < B; ++b) {
+                    const float hk = H1[(net * kPB + b) * kRow + lane];
+                    const float *z2 = H2 + (net * kPB + b) * kRow + j0;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc[u] = __builtin_fmaf(z2[u], hk, acc[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    G[(net ? L.vf2W : L.pi2W) + (j0 + u) * kHid + lane] = acc[u];
+            }
+            if (tid < 2 * kHid) {
+                const int net = tid >> 6, j = tid & 63;
+                const float *z2 = H2 + net * kPB * kRow + j;
+                float acc = 0.f;
+                for (int b = 0; b < B; ++b) acc += z2[b * kRow];
+                G[(net ? L.vf2b : L.pi2b) + j] = acc;
+            }
+            __syncthreads();
+            // ---- dL/dz1 in place of layer 1 (8 (net, b) pairs per wave, lane = k): one W2 read
+            // and 8 broadcast dL/dz2 reads per hidden row j
+            for (int grp = w; grp < 16; grp += kNW) {
+                const int net = (8 * grp) >> 6, b0 = (8 * grp) & 63;
+                if (b0 >= B) continue;
+                const float *w2 = W + (net ? L.vf2W : L.pi2W) + lane;
+                const float *z2 = H2 + (net * kPB + b0) * kRow;
+                float gh[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+                for (int j = 0; j < kHid; ++j) {
+                    const float wk = w2[j * kHid];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) gh[q] = __builtin_fmaf(wk, z2[q * kRow + j], gh[q]);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (b0 + q < B) {
+                        float *hp1 = H1 + (net * kPB + b0 + q) * kRow + lane;
+                        const float h = *hp1;
+                        *hp1 = gh[q] * (1.0f - h * h);
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- W1 gradients (one (net, j, i) per thread) and b1 gradients
+            for (int t = tid; t < 2 * kHid * 8; t += kPT) {
+                const int net = t >> 9, j = (t >> 3) & 63, i = t & 7;
+                if (i < D) {
+                    const float *z1 = H1 + net * kPB * kRow + j;
+                    float acc = 0.f;
+                    for (int b = 0; b < B; ++b) acc = __builtin_fmaf(z1[b * kRow], O[b * 9 + i], acc);
+                    G[(net ? L.vf0W : L.pi0W) + j * D + i] = acc;
+                }
+            }
+            if (tid < 2 * kHid) {
+                const int net = tid >> 6, j = tid & 63;
+                const float *z1 = H1 + net * kPB * kRow + j;
+                float acc = 0.f;
+                for (int b = 0; b < B; ++b) acc += z1[b * kRow];
+                G[(net ? L.vf0b : L.pi0b) + j] = acc;
+            }
+            __syncthreads();
+            // ---- clip_grad_norm_(max_grad_norm): global 2-norm
+            float ss = 0.f;
+#pragma unroll
+            for (int q = 0; q < kPerT; ++q) {
+                const int p = tid + q * kPT;
+                if (p < P) ss = __builtin_fmaf(G[p], G[p], ss);
+            }
+            ss = wsum(ss);
+            if (lane == 0) R[w] = ss;
+            __syncthreads();
+            float tot = 0.f;
+            for (int q = 0; q < kPT / 64; ++q) tot += R[q];
+            const float norm = __builtin_sqrtf(tot);
+            float coef = hp.max_grad_norm / (norm + 1e-6f);
+            coef = coef < 1.0f ? coef : 1.0f;
+            // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
+            step += 1.0f;
+            const float bc1 = 1.0f - powf(hp.beta1, step);
+            const float bc2 = 1.0f - powf(hp.beta2, step);
+            const float step_size = hp.lr / bc1;
+            const float bc2s = __builtin_sqrtf(bc2);
+#pragma unroll
+            for (int q = 0; q < kPerT; ++q) {
+                const int p = tid + q * kPT;
+                if (p < P) {
+                    const float gr = G[p] * coef;
+                    const float mq = m[p] + (1.0f - hp.beta1) * (gr - m[p]);
+                    const float vq = v[p] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
+                    m[p] = mq;
+                    v[p] = vq;
+                    const float den = __builtin_sqrtf(vq) / bc2s + hp.eps;
+                    W[p] = W[p] - step_size * (mq / den);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int p = tid; p < P; p += kPT) g.params[p] = W[p];
+    if (tid == 0) {
+        g.step[0] = step;
+        g.stats[0] += st_pl;
+        g.stats[1] += st_vl;
+        g.stats[2] += st_el;
+        g.stats[3] += st_cf;
+    }
+}
+
+hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
+                             int32_t D, const float *obs, const float *act,
+                             const float *old_log_prob, const float *adv, const float *ret,
+                             int64_t n, const int64_t *perm, int32_t n_epochs,
+                             int32_t batch_size, const ppo_hparams &hp, double *stats,
+                             hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_ppo_update),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kPPOLdsBytes);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    PPOArgs g{params, exp_avg, exp_avg_sq, step, obs, act, old_log_prob, adv, ret, perm, n,
+              D, n_epochs, batch_size, hp, stats};
+    hipLaunchKernelGGL(k_ppo_update, dim3(1), dim3(kPT), kPPOLdsBytes, st, g);
+    return hipGetLastError();
+}
+
+}  // namespace fenvk

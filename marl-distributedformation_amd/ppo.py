@@ -11,6 +11,7 @@ contiguous 9,669-float bucket: with several ranks it is all-reduced once per opt
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 
@@ -72,7 +73,7 @@ class PPO:
     """Minimal on-device PPO: collect (HIP kernels) -> GAE (HIP) -> clipped-surrogate update."""
 
     def __init__(self, env, cfg: PPOConfig | None = None, seed: int = 0, policy=None,
-                 use_graph: bool | None = None):
+                 use_graph: bool | None = None, use_fused: bool | None = None):
         self.cfg = cfg or PPOConfig()
         self.seed = int(seed)
         self.env = env
@@ -96,6 +97,9 @@ class PPO:
         self._k = torch.zeros((), dtype=torch.long, device=dev)
         self._sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self._graphs = None
+        # batch_size <= 64 (SB3's default 64): the whole update as one HIP kernel (ppo_update)
+        self.use_fused = ((self.param.device.type == "cuda" and self.world == 1
+                           and self.cfg.batch_size <= 64) if use_fused is None else use_fused)
 
     @property
     def num_timesteps(self) -> int:
@@ -176,11 +180,47 @@ class PPO:
                 self._graphs = (g1, None)
         torch.cuda.current_stream(self.param.device).wait_stream(s)
 
+    def _train_fused(self) -> dict:
+        """All epochs and minibatches in one ``ppo_update`` launch (csrc/ppo_update.hip): the
+        same randperm per epoch, losses, clipping and Adam (state kept in ``self.opt``)."""
+        from . import _lib
+        c = self.cfg
+        n = self.buffer.n_steps * self.buffer.n_envs
+        bs = min(int(c.batch_size), n)
+        dev = self.param.device
+        perm = torch.empty((c.n_epochs, n), dtype=torch.long, device=dev)
+        for e in range(c.n_epochs):
+            perm[e].copy_(torch.randperm(n, device=dev, generator=self.gen))
+        st = self.opt.state[self.param]
+        if not st:  # torch's capturable-Adam state layout, created before the first step
+            st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+            st["exp_avg"] = torch.zeros_like(self.param, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(self.param, memory_format=torch.preserve_format)
+        grp = self.opt.param_groups[0]
+        hp = _lib.PPOHParams(clip_range=c.clip_range, ent_coef=c.ent_coef, vf_coef=c.vf_coef,
+                             max_grad_norm=c.max_grad_norm, lr=float(grp["lr"]),
+                             beta1=float(grp["betas"][0]), beta2=float(grp["betas"][1]),
+                             eps=float(grp["eps"]), normalize_advantage=int(c.normalize_advantage))
+        obs, act, lp, adv, ret = (t.contiguous() for t in self._flat())
+        self._sums.zero_()
+        _lib.check(_lib.lib().ppo_update(
+            _lib.ptr(self.param), _lib.ptr(st["exp_avg"]), _lib.ptr(st["exp_avg_sq"]),
+            _lib.ptr(st["step"]), self.buffer.obs_dim, _lib.ptr(obs), _lib.ptr(act), _lib.ptr(lp),
+            _lib.ptr(adv), _lib.ptr(ret), n, _lib.ptr(perm), c.n_epochs, bs,
+            ctypes.byref(hp), _lib.ptr(self._sums), _lib.current_stream(dev)), "ppo_update")
+        steps = c.n_epochs * (-(-n // bs))
+        m = (self._sums / steps).tolist()
+        self.stats = dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2],
+                          clip_fraction=m[3])
+        return self.stats
+
     def train(self) -> dict:
         """SB3 ``PPO.train``: n_epochs over shuffled minibatches of the rollout buffer (the same
         randperm per epoch as ``RolloutBuffer.get``).  Full minibatches replay the captured
         graph(s); a trailing partial minibatch runs eagerly.  Losses are summed on the device and
         read once at the end."""
+        if self.use_fused and self.world == 1 and self.cfg.batch_size <= 64:
+            return self._train_fused()
         c = self.cfg
         n = self.buffer.n_steps * self.buffer.n_envs
         bs = min(int(c.batch_size), n)

@@ -108,3 +108,22 @@ def test_invalid_config_rejected(flib):
     assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.75, 1000, 0, 0, 0, 4) == -1
     assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.25, 1000, 0, 7, 0, 4) == -1
     assert L.fenv_create(ctypes.byref(h), 0, 4, 5, 1, 0.25, 1000, 0, 0, 2, 4) == -1
+
+
+def test_ppo_update_validates_before_launch(flib):
+    """ppo_update rejects bad arguments on the host (no kernel launch, no device needed)."""
+    L = flib.lib()
+    hp = flib.PPOHParams(clip_range=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, lr=1e-3,
+                         beta1=0.9, beta2=0.999, eps=1e-5, normalize_advantage=1)
+    fake = ctypes.c_void_p(0x1000)  # never dereferenced: validation fails first
+    args = [fake] * 4 + [8] + [fake] * 5 + [100, fake, 1, 64, ctypes.byref(hp), fake, None]
+    bad_bs = list(args)
+    bad_bs[13] = 65
+    assert L.ppo_update(*bad_bs) != 0
+    assert b"batch_size" in L.fenv_last_error()
+    bad_d = list(args)
+    bad_d[4] = 7
+    assert L.ppo_update(*bad_d) != 0
+    nul = list(args)
+    nul[0] = None
+    assert L.ppo_update(*nul) != 0

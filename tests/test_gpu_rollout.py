@@ -86,10 +86,12 @@ def test_torch_model_matches_kernel(mods):
     assert torch.allclose(ent, torch.full_like(ent, 2 * (0.5 + 0.5 * np.log(2 * np.pi))))
 
 
-def test_ppo_learns(mods):
+@pytest.mark.parametrize("batch_size,n_epochs", [(1024, 4), (64, 2)])  # graph / fused update
+def test_ppo_learns(mods, batch_size, n_epochs):
     cfg = {"num_formation": 256, "num_agents_per_formation": 5, "goal_in_obs": True}
     env = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=0, reset_mode="philox")
-    ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(batch_size=1024, n_epochs=4), seed=0)
+    ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(batch_size=batch_size, n_epochs=n_epochs),
+                          seed=0)
     before = ppo.policy.flat.clone()
     rewards = []
 
@@ -185,3 +187,34 @@ def test_graph_update_matches_eager(mods):
     torch.testing.assert_close(p1, p0, atol=1e-6, rtol=1e-5)
     for k in s0:
         assert abs(s0[k] - s1[k]) <= 1e-5 * max(1.0, abs(s0[k])), k
+
+
+@pytest.mark.parametrize("goal", [True, False])
+def test_fused_update_matches_torch(mods, goal):
+    """ppo_update (one HIP kernel for all epochs x minibatches: loss, backward, grad clip,
+    Adam) == the torch autograd update on the same samples and permutations, to fp32
+    summation-order rounding: 2 epochs x 13 minibatches of 64 (the last one 32)."""
+    cfg = {"num_formation": 16, "num_agents_per_formation": 5, "goal_in_obs": goal}
+    runs = []
+    for fused in (False, True):
+        env = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=1, reset_mode="philox")
+        ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(batch_size=64, n_epochs=2), seed=4,
+                              use_graph=False, use_fused=fused)
+        flat0 = ppo.policy.flat.clone()
+        for _ in range(2):
+            with torch.no_grad():
+                ppo.collector.collect()
+            st = ppo.train()
+        s = ppo.opt.state[ppo.param]
+        runs.append((flat0, ppo.policy.flat.clone(), st, s["exp_avg"].clone(),
+                     s["exp_avg_sq"].clone(), float(s["step"])))
+    (a0, p0, s0, m0, v0, k0), (a1, p1, s1, m1, v1, k1) = runs
+    assert torch.equal(a0, a1)
+    assert k0 == k1 == 2 * 2 * 13
+    moved = (p0 - a0).abs().max().item()
+    err = (p1 - p0).abs().max().item()
+    assert moved > 1e-3 and err < 1e-3 * moved, (moved, err)
+    torch.testing.assert_close(m1, m0, atol=1e-6, rtol=1e-3)
+    torch.testing.assert_close(v1, v0, atol=1e-9, rtol=1e-3)
+    for k in s0:
+        assert abs(s0[k] - s1[k]) <= 1e-4 * max(1.0, abs(s0[k])), (k, s0[k], s1[k])
