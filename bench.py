@@ -144,6 +144,45 @@ def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: 
             "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
+                     updates: int = 2) -> dict:
+    """Secondary measurement: SB3's PPO.train at the reference's training config
+    (vectorized_env.py:126-131: n_steps 10, batch 64, 10 epochs over 1000 x 5 agents) with the
+    fused ppo_update kernel; one update = 7,820 minibatch steps."""
+    import torch
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    ppo_mod = import_module(pkgname + ".ppo")
+    cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode="philox")
+    m = ppo_mod.PPO(env, ppo_mod.PPOConfig(), seed=0)
+    with torch.no_grad():
+        m.collector.collect()
+    m.train()  # warm-up (allocates the Adam state)
+    torch.cuda.synchronize()
+    el = 0.0
+    for _ in range(updates):
+        with torch.no_grad():
+            m.collector.collect()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m.train()
+        torch.cuda.synchronize()
+        el += time.perf_counter() - t0
+    n = env.num_envs * m.cfg.n_steps
+    mb = m.cfg.n_epochs * -(-n // m.cfg.batch_size)
+    per_mb = el / (updates * mb)
+    flop = 56448.0 * m.cfg.batch_size  # ~3 x 18,816 FLOP per sample (forward + backward)
+    return {"workload": f"PPO.train, {formations} x {agents} agents, n_steps 10, batch 64, "
+                        f"10 epochs (SB3 defaults of the reference's PPO call)",
+            "path": "fused" if m.use_fused else ("graph" if m.use_graph else "eager"),
+            "ms_per_update": el / updates * 1e3, "us_per_minibatch": per_mb * 1e6,
+            "samples_per_s": n * m.cfg.n_epochs / (el / updates),
+            "gflops": flop / per_mb / 1e9,
+            "note": "one workgroup (a minibatch depends on the previous one's parameters); "
+                    "single-CU fp32 peak is ~614 GFLOP/s"}
+
+
 def load_pmc_traffic(workload: str):
     """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -308,6 +347,8 @@ def main():
                                     "every_rollouts": args.stats_every}
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
+        if world == 1 and not args.no_policy:
+            out["ppo_update"] = ppo_update_bench(pkg.__name__, dev)
         if world == 1 and not args.no_configs:
             out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
                                   "config4": env_config_bench(pkg.__name__, dev, 16384, 64)}
