@@ -115,7 +115,7 @@ FIELDS = ("observations", "actions", "clipped", "mu", "values", "log_probs", "re
     (1001, 10, True, 10, "philox", 23, False),   # BASELINE config-2 shape (scaled), tail wave
     (37, 64, True, 6, "mt19937", 9, False),      # one formation per wavefront
     (50, 7, False, 8, "philox", 11, True),       # D = 6, 9 formations / wave, deterministic
-    (40, 5, True, 20, "philox", 7, False),       # T > 16: GAE as a separate launch
+    (40, 5, True, 20, "philox", 7, False),       # T = 20: long rollout, several resets
     (9, 33, True, 3, "mt19937", 1000, False),    # M = 33: second tile has one agent
 ])
 def test_fused_rollout_matches_unfused(mods, F, N, goal, T, mode, max_steps, det):

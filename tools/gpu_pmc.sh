@@ -4,7 +4,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${TAG:-r1}
-ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline --no-stats --no-policy}
+ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline --no-stats --no-policy --no-configs}
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$R/gpurun_out/pmc_${TAG}_$C" -o pmc \
