@@ -9,9 +9,9 @@
 // Why one workgroup: a minibatch step depends on the previous step's parameters, and a 64-sample
 // step of this 9,669-parameter MLP is ~1.8 MFLOP -- far too little to spread over the chip, and
 // ~100 tiny launches per step in torch (~430 us replayed as a HIP graph).  Here the parameters,
-// their gradients and the minibatch's activations live in LDS (151 KB), the Adam moments stay in
-// (L2-resident) global memory, and the loop runs every minibatch of every epoch inside one
-// launch.  The three 64-deep contractions are register-blocked 8 ways so a multiply-add costs
+// their gradients and the minibatch's activations live in LDS (151 KB), each thread keeps the
+// Adam moments of the ~19 parameters it owns in registers, and the loop runs every minibatch of
+// every epoch inside one launch.  The three 64-deep contractions are register-blocked 8 ways so a multiply-add costs
 // ~1 LDS read instead of 2.  All arithmetic is fp32 VALU (fmaf chains); results match the torch
 // path to summation-order rounding (tests/test_gpu_rollout.py).
 //
@@ -70,6 +70,20 @@ __device__ __forceinline__ float wsum(float v) {
     return v;
 }
 
+#ifndef FENV_PPO_PROFILE
+#define FENV_PPO_PROFILE 0  // 1: per-phase shader-clock totals -> stats[4..15] (diagnostic build)
+#endif
+#if FENV_PPO_PROFILE
+#define FENV_PPO_PHASE(i)                                            \
+    if (tid == 0) {                                                  \
+        const uint64_t now = __builtin_readcyclecounter();           \
+        prof[i] += (double)(now - tlast);                            \
+        tlast = now;                                                 \
+    }
+#else
+#define FENV_PPO_PHASE(i)
+#endif
+
 __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *W = sm + oPW, *G = sm + oPG, *O = sm + oPO, *H1 = sm + oPH1, *H2 = sm + oPH2;
@@ -82,10 +96,20 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
     const ppo_hparams hp = g.hp;
 
     for (int p = tid; p < P; p += kPT) W[p] = g.params[p];
-    float *__restrict__ m = g.exp_avg;  // Adam moments stay in global memory (L2-resident)
-    float *__restrict__ v = g.exp_avg_sq;
+    float m[kPerT], v[kPerT];  // Adam moments of the parameters this thread owns
+#pragma unroll
+    for (int q = 0; q < kPerT; ++q) {
+        const int p = tid + q * kPT;
+        m[q] = p < P ? g.exp_avg[p] : 0.0f;
+        v[q] = p < P ? g.exp_avg_sq[p] : 0.0f;
+    }
     float step = g.step[0];
+    const float lb1 = log2f(hp.beta1), lb2 = log2f(hp.beta2);
     double st_pl = 0.0, st_vl = 0.0, st_el = 0.0, st_cf = 0.0;
+#if FENV_PPO_PROFILE
+    double prof[11] = {};
+    uint64_t tlast = __builtin_readcyclecounter();
+#endif
     __syncthreads();
 
     const int64_t n = g.n;
@@ -110,6 +134,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 S[sRET * kPB + b] = g.ret[r];
             }
             __syncthreads();
+            FENV_PPO_PHASE(0);
             // ---- advantage normalisation (wave 0) || layer 1 (all waves)
             if (w == 0 && hp.normalize_advantage && B > 1) {
                 const float a = lane < B ? S[sADV * kPB + lane] : 0.0f;
@@ -123,11 +148,14 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     const int net = u >> 6, j = u & 63;
                     const float *w1 = W + (net ? L.vf0W : L.pi0W) + j * D;
                     float z = W[(net ? L.vf0b : L.pi0b) + j];
-                    for (int i = 0; i < D; ++i) z = __builtin_fmaf(w1[i], O[lane * 9 + i], z);
+                    // 8 terms always: obs is zero-padded past D, so the extra w1[i] * 0 add nothing
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) z = __builtin_fmaf(w1[i], O[lane * 9 + i], z);
                     H1[(net * kPB + lane) * kRow + j] = tanhf(z);
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(1);
             // ---- layer 2: lane = sample, 8 units per wave; per 4 k one h read per k and one
             // broadcast ds_read_b128 of W2 per unit (the fmaf chain over k keeps its order)
             for (int grp = w; grp < 16 && lane < B; grp += kNW) {
@@ -137,7 +165,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 float acc[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) acc[u] = W[(net ? L.vf2b : L.pi2b) + j0 + u];
-#pragma unroll 1
+#pragma unroll 4
                 for (int k = 0; k < kHid; k += 4) {
                     const float h0 = h[k], h1 = h[k + 1], h2 = h[k + 2], h3 = h[k + 3];
 #pragma unroll
@@ -153,6 +181,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 for (int u = 0; u < 8; ++u) H2[(net * kPB + lane) * kRow + j0 + u] = tanhf(acc[u]);
             }
             __syncthreads();
+            FENV_PPO_PHASE(2);
             // ---- heads, losses and per-sample gradients (wave 0, lane = sample)
             if (w == 0) {
                 const bool on = lane < B;
@@ -224,15 +253,18 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(3);
             // ---- head weight gradients (waves 0-2, lane = hidden unit k)
             if (w < 3) {
                 const int slot = w == 0 ? sGMU0 : (w == 1 ? sGMU1 : sGV);
                 const float *h = H2 + (w == 2 ? kPB : 0) * kRow;
                 float acc = 0.f;
+#pragma unroll 8
                 for (int b = 0; b < B; ++b) acc = __builtin_fmaf(S[slot * kPB + b], h[b * kRow + lane], acc);
                 G[(w == 2 ? L.valW : L.actW + w * kHid) + lane] = acc;
             }
             __syncthreads();
+            FENV_PPO_PHASE(4);
             // ---- dL/dz2 in place (pairs (net, b): wave w handles 8 of them, lane = k)
             for (int pr = w; pr < 2 * kPB; pr += kNW) {
                 const int net = pr >> 6, b = pr & 63;
@@ -246,12 +278,13 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(5);
             // ---- W2 gradients (rows (net, j0..j0+7) per wave, lane = k): one h1 read and 8
             // broadcast dL/dz2 reads per sample
             for (int grp = w; grp < 16; grp += kNW) {
                 const int net = (8 * grp) >> 6, j0 = (8 * grp) & 63;
                 float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
+#pragma unroll 8
                 for (int b = 0; b < B; ++b) {
                     const float hk = H1[(net * kPB + b) * kRow + lane];
                     const float *z2 = H2 + (net * kPB + b) * kRow + j0;
@@ -266,10 +299,12 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const int net = tid >> 6, j = tid & 63;
                 const float *z2 = H2 + net * kPB * kRow + j;
                 float acc = 0.f;
+#pragma unroll 8
                 for (int b = 0; b < B; ++b) acc += z2[b * kRow];
                 G[(net ? L.vf2b : L.pi2b) + j] = acc;
             }
             __syncthreads();
+            FENV_PPO_PHASE(6);
             // ---- dL/dz1 in place of layer 1 (8 (net, b) pairs per wave, lane = k): one W2 read
             // and 8 broadcast dL/dz2 reads per hidden row j
             for (int grp = w; grp < 16; grp += kNW) {
@@ -278,7 +313,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const float *w2 = W + (net ? L.vf2W : L.pi2W) + lane;
                 const float *z2 = H2 + (net * kPB + b0) * kRow;
                 float gh[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
+#pragma unroll 8
                 for (int j = 0; j < kHid; ++j) {
                     const float wk = w2[j * kHid];
 #pragma unroll
@@ -294,12 +329,14 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(7);
             // ---- W1 gradients (one (net, j, i) per thread) and b1 gradients
             for (int t = tid; t < 2 * kHid * 8; t += kPT) {
                 const int net = t >> 9, j = (t >> 3) & 63, i = t & 7;
                 if (i < D) {
                     const float *z1 = H1 + net * kPB * kRow + j;
                     float acc = 0.f;
+#pragma unroll 8
                     for (int b = 0; b < B; ++b) acc = __builtin_fmaf(z1[b * kRow], O[b * 9 + i], acc);
                     G[(net ? L.vf0W : L.pi0W) + j * D + i] = acc;
                 }
@@ -308,10 +345,12 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const int net = tid >> 6, j = tid & 63;
                 const float *z1 = H1 + net * kPB * kRow + j;
                 float acc = 0.f;
+#pragma unroll 8
                 for (int b = 0; b < B; ++b) acc += z1[b * kRow];
                 G[(net ? L.vf0b : L.pi0b) + j] = acc;
             }
             __syncthreads();
+            FENV_PPO_PHASE(8);
             // ---- clip_grad_norm_(max_grad_norm): global 2-norm
             float ss = 0.f;
 #pragma unroll
@@ -322,6 +361,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             ss = wsum(ss);
             if (lane == 0) R[w] = ss;
             __syncthreads();
+            FENV_PPO_PHASE(9);
             float tot = 0.f;
             for (int q = 0; q < kPT / 64; ++q) tot += R[q];
             const float norm = __builtin_sqrtf(tot);
@@ -329,8 +369,8 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             coef = coef < 1.0f ? coef : 1.0f;
             // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
             step += 1.0f;
-            const float bc1 = 1.0f - powf(hp.beta1, step);
-            const float bc2 = 1.0f - powf(hp.beta2, step);
+            const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
+            const float bc2 = 1.0f - exp2f(step * lb2);
             const float step_size = hp.lr / bc1;
             const float bc2s = __builtin_sqrtf(bc2);
 #pragma unroll
@@ -338,24 +378,34 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const int p = tid + q * kPT;
                 if (p < P) {
                     const float gr = G[p] * coef;
-                    const float mq = m[p] + (1.0f - hp.beta1) * (gr - m[p]);
-                    const float vq = v[p] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
-                    m[p] = mq;
-                    v[p] = vq;
-                    const float den = __builtin_sqrtf(vq) / bc2s + hp.eps;
-                    W[p] = W[p] - step_size * (mq / den);
+                    m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
+                    v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
+                    const float den = __builtin_sqrtf(v[q]) / bc2s + hp.eps;
+                    W[p] = W[p] - step_size * (m[q] / den);
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(10);
         }
     }
     for (int p = tid; p < P; p += kPT) g.params[p] = W[p];
+#pragma unroll
+    for (int q = 0; q < kPerT; ++q) {
+        const int p = tid + q * kPT;
+        if (p < P) {
+            g.exp_avg[p] = m[q];
+            g.exp_avg_sq[p] = v[q];
+        }
+    }
     if (tid == 0) {
         g.step[0] = step;
         g.stats[0] += st_pl;
         g.stats[1] += st_vl;
         g.stats[2] += st_el;
         g.stats[3] += st_cf;
+#if FENV_PPO_PROFILE
+        for (int q = 0; q < 11; ++q) g.stats[4 + q] += prof[q];
+#endif
     }
 }
 
