@@ -3,8 +3,11 @@
 
 Metric (BASELINE.json): agent-steps/sec (whole node) at 5 agents/formation, and the step
 kernel's fraction of the HBM roofline.  Workload: BASELINE config 3 -- 1,048,576 formations x 5
-agents (5,242,880 agents), sharded contiguously over the ranks (strong scaling: the same batch
-on 1, 2, 4 or 8 GPUs).  A "step" is one env step of every agent; steps run as fused rollouts of
+agents (5,242,880 agents) per GPU.  Formations are independent, so the ranks own disjoint
+contiguous formation shards of one global env with no data-path collective (weak scaling: N
+GPUs step N x 1M formations; `--strong` instead splits `--formations` over the ranks, i.e. config
+3's literal 1M formations over 8 GPUs, and tools/shard_sizes.sh measures those shard sizes on
+one GPU).  A "step" is one env step of every agent; steps run as fused rollouts of
 `--chunk` steps per launch (SB3's n_steps=10 rollout, vectorized_env.py:128) writing obs /
 reward / done for every step into a device rollout buffer, with the actions read from HBM
 (inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
@@ -202,7 +205,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--formations", type=int, default=1 << 20)
+    ap.add_argument("--formations", type=int, default=1 << 20,
+                    help="formations per GPU (weak scaling), or in total with --strong")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: shard --formations over the ranks")
     ap.add_argument("--agents", type=int, default=5)
     ap.add_argument("--chunk", type=int, default=10)
     ap.add_argument("--reset-mode", default="philox", choices=["philox", "mt19937"])
@@ -236,10 +242,11 @@ def main():
 
     N, T = args.agents, args.chunk
     D = 6 if args.no_goal else 8
-    first, F = pdist.shard_range(args.formations, rank, world)
+    total_formations = args.formations if args.strong else args.formations * world
+    first, F = pdist.shard_range(total_formations, rank, world)
     cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": not args.no_goal}
     env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode=args.reset_mode,
-                            first_formation=first, total_formations=args.formations)
+                            first_formation=first, total_formations=total_formations)
     A = F * N
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     acts = [(torch.rand((T, A, 2), device=dev, generator=g) * 2 - 1) for _ in range(2)]
@@ -307,12 +314,12 @@ def main():
     elapsed = pdist.max_over_ranks(elapsed, dev)
     kern_avg_ms = pdist.max_over_ranks(kern_avg_ms, dev)
 
-    total_agents = args.formations * N
+    total_agents = total_formations * N
     value = total_agents * steps / elapsed
     bytes_launch = rollout_bytes_per_launch(A, N, D, T)
     achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
-    workload = (f"config3: {args.formations} formations x {N} agents, fused {T}-step "
-                f"rollouts, {args.reset_mode} resets")
+    workload = (f"config3: {total_formations} formations x {N} agents "
+                f"({F} per GPU x {world}), fused {T}-step rollouts, {args.reset_mode} resets")
     traffic, tsrc = load_pmc_traffic(workload if world == 1 else "")
     if rank == 0:
         out = {
@@ -324,11 +331,11 @@ def main():
             "warmup": warm_chunks * T,
             "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: U(-1,1) fp32 actions resident in HBM, random-init formations",
-            "config": {"workload": workload, "formations": args.formations,
+            "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
                        "parallelism": f"formation-shard dp{world}"},

@@ -222,7 +222,7 @@ int fenv_info(const fenv_t *e, int64_t *o) {
     return FENV_OK;
 }
 
-int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::group_count(e->c) : -1; }
+int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::rollout_group_count(e->c) : -1; }
 
 int fenv_reset(fenv_t *e, float *obs, void *stream) {
     if (!e) return fail(FENV_EINVAL, "fenv_reset: NULL handle");

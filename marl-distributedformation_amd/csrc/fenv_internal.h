@@ -38,7 +38,9 @@ struct Consts {
 // Geometry: N <= 64 -> `fpw` whole formations per wavefront, 256-thread workgroups.
 //           N  > 64 -> one formation per workgroup of round_up(N, 64) threads (LDS exchange).
 inline bool wave_path(int32_t N) { return N <= 64; }
-int64_t group_count(const Consts &c);  // wavefronts (N<=64) or workgroups (N>64)
+int64_t group_count(const Consts &c);  // 4-wave workgroups (N<=64) or formations (N>64)
+// workgroups of the rollout/step launch = records of its stats partials
+int64_t rollout_group_count(const Consts &c);
 
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,

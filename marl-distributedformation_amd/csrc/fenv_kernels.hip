@@ -178,6 +178,187 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     }
 }
 
+// ---------------------------------------------------------------- workgroup-staged rollout (N <= 64)
+// Compute mapping of rollout_body (a wave holds fpw whole formations, lane = agent, ring
+// exchanges are wave shuffles, state in registers for the T steps); memory traffic per
+// WORKGROUP: kRW waves cover one contiguous agent slice whose actions come in and whose
+// obs / reward / done rows go out through LDS as contiguous full-width accesses, one barrier per
+// step (double-buffered).  At N = 5 or 10 a slice is 480 agents = whole 128-B lines of every
+// stream, where per-wave 60-agent rows straddle lines (tools/ubench_hbm.hip 'wgstage 480').
+#ifndef FENV_RW_OCC
+#define FENV_RW_OCC
+#endif
+#ifndef FENV_RW
+#define FENV_RW 0  // 1: use k_rollout_wg for N <= 64 (A/B against k_rollout_wave)
+#endif
+#ifndef FENV_RW_K
+#define FENV_RW_K 8
+#endif
+#ifndef FENV_RW_OBSBUF
+#define FENV_RW_OBSBUF 2  // 1: one obs stage + a second barrier per step (less LDS, more WGs/CU)
+#endif
+constexpr int kRW = FENV_RW_K;
+constexpr int kRWA = 64 * kRW;
+constexpr int kOB = FENV_RW_OBSBUF;
+
+struct RWLds {  // dynamic LDS layout, in floats
+    static constexpr int act = 0;                       // [2][kRWA] float2
+    static constexpr int rew = act + 2 * 2 * kRWA;      // [2][kRWA] float
+    static constexpr int done = rew + 2 * kRWA;         // [2][kRWA] uint8
+    static constexpr int red = done + 2 * (kRWA / 4);   // [kRW] float2
+    static constexpr int obs = red + 2 * kRW;           // [2][kRWA * D] float
+    static constexpr size_t bytes(int D) { return (size_t)(obs + kOB * kRWA * D) * sizeof(float); }
+};
+
+template <int D, int MODE>
+__global__ __launch_bounds__(64 * kRW) FENV_RW_OCC void k_rollout_wg(Consts c, DevState st,
+                                                                     DevPending p, int32_t T,
+                                                                     const float2 *__restrict__ act,
+                                                                     float *__restrict__ obs,
+                                                                     float *__restrict__ rew,
+                                                                     uint8_t *__restrict__ done,
+                                                                     float2 *__restrict__ partial,
+                                                                     bool accum) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float2 *s_act = reinterpret_cast<float2 *>(lds + RWLds::act);
+    float *s_rew = lds + RWLds::rew;
+    uint8_t *s_done = reinterpret_cast<uint8_t *>(lds + RWLds::done);
+    float2 *s_red = reinterpret_cast<float2 *>(lds + RWLds::red);
+    float *s_obs = lds + RWLds::obs;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int N = c.N;
+    const int M = c.fpw * N;
+    const int fi = lane / N;
+    const int i = lane - fi * N;
+    const int64_t wave = (int64_t)blockIdx.x * kRW + w;
+    const int64_t f = wave * c.fpw + fi;
+    const bool active = fi < c.fpw && f < c.F;
+    const int64_t a = f * N + i;
+    const int li = w * M + lane;
+    const WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
+    const int64_t A = c.F * (int64_t)N;
+    const int64_t g0 = (int64_t)blockIdx.x * kRW * M;
+    const int nwg = (int)((A - g0) < (int64_t)kRW * M ? (A - g0) : (int64_t)kRW * M);
+    const bool a4 = ((A | g0 | (int64_t)nwg) & 1) == 0;  // slice loads as float4 (2 agents)
+    const int nld = a4 ? (nwg >> 1) : nwg;
+
+    Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
+    if (active) {
+        s.px = st.px[a];
+        s.py = st.py[a];
+        s.gx = st.gx[f];
+        s.gy = st.gy[f];
+        s.t = st.t[f];
+        s.ep = st.ep[f];
+    }
+    bool any_reset = false;
+    float rsum = 0.f, dsum = 0.f;
+    float4 nxt = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < nld) {
+        if (a4) nxt = reinterpret_cast<const float4 *>(act + g0)[tid];
+        else nxt = make_float4(act[g0 + tid].x, act[g0 + tid].y, 0.f, 0.f);
+        if (a4) reinterpret_cast<float4 *>(s_act)[tid] = nxt;
+        else s_act[tid] = make_float2(nxt.x, nxt.y);
+    }
+    __syncthreads();
+    for (int32_t k = 0; k < T; ++k) {
+        const int b = k & 1;
+        if (k + 1 < T && tid < nld) {  // next step's slice, in flight during this step
+            const float2 *src = act + (int64_t)(k + 1) * A + g0;
+            if (a4) nxt = reinterpret_cast<const float4 *>(src)[tid];
+            else nxt = make_float4(src[tid].x, src[tid].y, 0.f, 0.f);
+        }
+        const float2 ac = active ? s_act[b * kRWA + li] : make_float2(0.f, 0.f);
+        float rw;
+        bool dn, rs;
+        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        any_reset |= rs;
+        float o[8];
+        env_obs<D>(x, s, o);
+        if (kOB == 1 && k > 0) __syncthreads();  // previous step's obs writeback has drained
+        if (active) {
+            float *row = s_obs + (size_t)(kOB == 2 ? b : 0) * kRWA * D + li * D;
+            if (D == 8) {
+                reinterpret_cast<float4 *>(row)[0] = make_float4(o[0], o[1], o[2], o[3]);
+                reinterpret_cast<float4 *>(row)[1] = make_float4(o[4], o[5], o[6], o[7]);
+            } else {
+                reinterpret_cast<float2 *>(row)[0] = make_float2(o[0], o[1]);
+                reinterpret_cast<float2 *>(row)[1] = make_float2(o[2], o[3]);
+                reinterpret_cast<float2 *>(row)[2] = make_float2(o[4], o[5]);
+            }
+            s_rew[b * kRWA + li] = rw;
+            s_done[b * kRWA + li] = (uint8_t)dn;
+            rsum += rw;
+            dsum += dn ? 1.0f : 0.0f;
+        }
+        if (k + 1 < T && tid < nld) {
+            if (a4) reinterpret_cast<float4 *>(s_act + (b ^ 1) * kRWA)[tid] = nxt;
+            else s_act[(b ^ 1) * kRWA + tid] = make_float2(nxt.x, nxt.y);
+        }
+        __syncthreads();
+        const int64_t row0 = (int64_t)k * A + g0;
+        if (obs) {
+            const float *src = s_obs + (size_t)(kOB == 2 ? b : 0) * kRWA * D;
+            float *dst = obs + row0 * D;
+            const int nf = nwg * D;
+            if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && (nf & 3) == 0) {
+#pragma unroll 1
+                for (int q = tid; q < (nf >> 2); q += 64 * kRW)
+                    reinterpret_cast<float4 *>(dst)[q] = reinterpret_cast<const float4 *>(src)[q];
+            } else {
+#pragma unroll 1
+                for (int q = tid; q < (nf >> 1); q += 64 * kRW)
+                    reinterpret_cast<float2 *>(dst)[q] = reinterpret_cast<const float2 *>(src)[q];
+            }
+        }
+        if (rew) {
+            const float *src = s_rew + b * kRWA;
+            float *dst = rew + row0;
+            if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && (nwg & 3) == 0) {
+                if (tid < (nwg >> 2))
+                    reinterpret_cast<float4 *>(dst)[tid] = reinterpret_cast<const float4 *>(src)[tid];
+            } else {
+                if (tid < nwg) dst[tid] = src[tid];
+            }
+        }
+        if (done) {
+            const uint8_t *src = s_done + b * kRWA;
+            uint8_t *dst = done + row0;
+            if (((reinterpret_cast<uintptr_t>(dst) & 3) == 0) && (nwg & 3) == 0) {
+                if (tid < (nwg >> 2))
+                    reinterpret_cast<uint32_t *>(dst)[tid] = reinterpret_cast<const uint32_t *>(src)[tid];
+            } else {
+                if (tid < nwg) dst[tid] = src[tid];
+            }
+        }
+    }
+    if (active) {
+        st.px[a] = s.px;
+        st.py[a] = s.py;
+        if (i == 0) {
+            st.t[f] = s.t;
+            if (any_reset) {
+                st.gx[f] = s.gx;
+                st.gy[f] = s.gy;
+                st.ep[f] = s.ep;
+            }
+        }
+    }
+    if (partial) {
+        rsum = wave_sum(rsum);
+        dsum = wave_sum(dsum);
+        if (lane == 0) s_red[w] = make_float2(rsum, dsum);
+        __syncthreads();
+        if (tid == 0) {
+            float2 v = s_red[0];
+            for (int q = 1; q < kRW; ++q) v = make_float2(v.x + s_red[q].x, v.y + s_red[q].y);
+            if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
+            partial[blockIdx.x] = v;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- reset + observe
 template <int D, int MODE, bool RESET, class X>
 __device__ __forceinline__ void reset_obs_body(const Consts &c, const DevState &st,
@@ -378,6 +559,11 @@ int64_t group_count(const Consts &c) {
     return c.F;
 }
 
+int64_t rollout_group_count(const Consts &c) {
+    if (FENV_RW && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
+    return group_count(c);
+}
+
 static inline unsigned block_threads(int32_t N) { return (unsigned)((N + 63) / 64 * 64); }
 
 template <int D, int MODE>
@@ -386,7 +572,11 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
                              float *partial, bool accum, hipStream_t st) {
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
-    if (wave_path(c.N)) {
+    if (FENV_RW && wave_path(c.N)) {
+        hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
+                           dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
+                           accum);
+    } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
         hipLaunchKernelGGL((k_rollout_wave<D, MODE>), dim3(blocks), dim3(256), 0, st, c, s, p, T,
                            a2, obs, rew, done, p2, accum);

@@ -7,7 +7,7 @@ run() {
   timeout -k 10 120 python bench.py --no-cpu-baseline --no-policy --no-configs --steps ${STEPS:-2000} --warmup 100 ${ARGS:-} 2>/dev/null |
     python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(f\"{r['avg_kernel_ms']*1e3:.1f} us  {r['achieved']:.0f} GB/s  frac {r['frac']:.3f}  value {d['value']:.4g}\")"
 }
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   echo "in-tree: $(run)" || exit 1
   for lib in build_variants/libfenv_*.so; do
     [ -e "$lib" ] || continue

@@ -31,7 +31,7 @@ if not fetch or not write:
 f_kb = sum(fetch) / len(fetch)
 w_kb = sum(write) / len(write)
 res = {
-    "workload": "config3: 1048576 formations x 5 agents, fused 10-step rollouts, philox resets",
+    "workload": "config3: 1048576 formations x 5 agents (1048576 per GPU x 1), fused 10-step rollouts, philox resets",
     "kernel": "k_rollout_wave",
     "dispatches": [len(fetch), len(write)],
     "FETCH_SIZE_kib_per_launch": f_kb,
