@@ -12,6 +12,7 @@ contiguous 9,669-float bucket: with several ranks it is all-reduced once per opt
 from __future__ import annotations
 
 import ctypes
+import gc
 import math
 from dataclasses import dataclass
 
@@ -22,6 +23,18 @@ import torch.nn.functional as Fn
 from . import checkpoint as ckpt
 from .policy import MlpPolicy
 from .rollout import RolloutBuffer, RolloutCollector
+
+_CAPTURE_STREAMS: dict = {}
+
+
+def _capture_stream(device: torch.device) -> torch.cuda.Stream:
+    """One capture stream per device for every PPO instance of the process: a fresh stream per
+    capture made the 8th capture in one process fail inside hipBLASLt
+    (tools/graph_capture_probe.py)."""
+    key = torch.device(device).index
+    if key not in _CAPTURE_STREAMS:
+        _CAPTURE_STREAMS[key] = torch.cuda.Stream(device)
+    return _CAPTURE_STREAMS[key]
 
 
 @dataclass
@@ -155,7 +168,11 @@ class PPO:
         # the replay would gather with garbage indices): attributes, not locals
         self._ar = torch.arange(bs, device=self.param.device)
         ar = self._ar
-        s = torch.cuda.Stream(self.param.device)
+        # Graphs of PPO objects that are unreachable but still in reference cycles stay alive
+        # until the cycle collector runs; with 7 of them alive the next capture fails inside
+        # hipBLASLt (tools/graph_capture_probe.py, PROBE_GC=1 clears it).  Free them first.
+        gc.collect()
+        s = _capture_stream(self.param.device)
         s.wait_stream(torch.cuda.current_stream(self.param.device))
         with torch.cuda.stream(s):
             for idx in warm_idx:
