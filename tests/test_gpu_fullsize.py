@@ -1,0 +1,178 @@
+"""GPU parity at BASELINE.json's full sizes (configs 1-4: 4,096 x 5, 65,536 x 10, 1,048,576 x 5,
+16,384 x 64), where the CPU oracle cannot replay the whole batch in seconds.
+
+Formations are independent (no cross-formation term in simulate.py:150-236), so a sample of
+formations -- random ones plus the first and last two, i.e. the grid's first wavefront and its
+partial last one -- is replayed by the C oracle from the GPU's own state and actions and must
+match bit for bit over a fused 10-step rollout (the bench's launch).  Size-independent checks
+cover the rest of the arrays: the per-workgroup {reward, done} records reduce to the sums of the
+full reward/done arrays (checksum of checksums), the last observation is the final state
+normalised (simulate.py:156-160) for every agent, and no agent moved more than 10 px per axis per
+step (vectorized_env.py:69-70 with |a| <= 1.2)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import COracleEnv
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+T = 10
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+@pytest.mark.parametrize("F,N,goal", [(4096, 5, True), (65536, 10, True), (1 << 20, 5, True),
+                                      (1 << 20, 5, False), (16384, 64, True)])
+def test_full_size_sampled_vs_oracle(venv, F, N, goal):
+    env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                             "goal_in_obs": goal}, device=DEV, seed=21, reset_mode="philox")
+    A, D = F * N, env.obs_dim
+    env.reset_tensor()
+    g = torch.Generator(device=DEV).manual_seed(F + N)
+    env.rollout(torch.rand((T, A, 2), device=DEV, generator=g) * 2.4 - 1.2)  # varied state, t > 0
+    px0, py0, gx0, gy0, t0 = env.get_state()
+    acts = torch.rand((T, A, 2), device=DEV, generator=g) * 2.4 - 1.2
+    part = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
+    obs, rew, done = env.rollout(acts, partial=part)
+    sums = env.reduce_partials(part).cpu().numpy()
+    px1, py1, gx1, gy1, t1 = env.get_state()
+    torch.cuda.synchronize()
+
+    rng = np.random.default_rng(F * 131 + N)
+    fs = np.unique(np.concatenate([rng.choice(F, min(F, 3000), replace=False),
+                                   [0, 1, F - 2, F - 1]]))
+    ag = (fs[:, None] * N + np.arange(N)).reshape(-1)
+    agt, fst = torch.from_numpy(ag).to(DEV), torch.from_numpy(fs).to(DEV)
+    ref = COracleEnv(len(fs), N, goal, 0)
+    ref.set_state(*(v[agt].cpu().numpy() for v in (px0, py0)),
+                  *(v[fst].cpu().numpy() for v in (gx0, gy0, t0)))
+    a_s = acts[:, agt].cpu().numpy()
+    o_s, r_s, d_s = obs[:, agt].cpu().numpy(), rew[:, agt].cpu().numpy(), done[:, agt].cpu().numpy()
+    for j in range(T):
+        ro, rr, rd, _ = ref.step(np.ascontiguousarray(a_s[j]))
+        assert np.array_equal(bits(o_s[j]), bits(ro)), f"obs step {j}"
+        assert np.array_equal(bits(r_s[j]), bits(rr)), f"reward step {j}"
+        assert np.array_equal(d_s[j], rd), f"done step {j}"
+    rs = ref.get_state()
+    for name, v, w, idx in (("px", px1, rs[0], agt), ("py", py1, rs[1], agt),
+                            ("gx", gx1, rs[2], fst), ("gy", gy1, rs[3], fst),
+                            ("t", t1, rs[4], fst)):
+        assert np.array_equal(bits(v[idx].cpu().numpy()), bits(w)), name
+
+    # checksum of checksums: the stats records cover every agent-step exactly once
+    rsum = rew.double().sum().item()
+    assert abs(sums[0] - rsum) <= 1e-5 * max(1.0, abs(rsum)), (sums[0], rsum)
+    assert sums[1] == float(done.sum().item())
+    # the last observation is the final state, normalised, for every agent
+    p1x, p1y = px1.cpu().numpy(), py1.cpu().numpy()
+    last = obs[-1].cpu().numpy()
+    assert np.array_equal(bits(last[:, 0]), bits(p1x / np.float32(400.0)))
+    assert np.array_equal(bits(last[:, 1]), bits(p1y / np.float32(600.0)))
+    if goal:
+        gxa = np.repeat(gx1.cpu().numpy(), N)
+        assert np.array_equal(bits(last[:, 6]), bits((gxa - p1x) / np.float32(400.0)))
+    # kinematics bound and no timeout inside these 20 steps (episode = 1002 steps)
+    p0x = px0.cpu().numpy()
+    assert np.abs(p1x - p0x).max() <= 10 * 1.2 * T + 1e-3
+    assert not done.any().item() and np.all(t1.cpu().numpy() == 2 * T)
+
+
+def _normals(rows: np.ndarray, seed: int, offset: int) -> np.ndarray:
+    """policy_oracle.philox_normals for selected rows (the kernel keys the noise by agent row)."""
+    import math
+
+    import policy_oracle as po
+    r64 = rows.astype(np.uint64)
+    ctr = np.stack([r64 & np.uint64(0xFFFFFFFF), r64 >> np.uint64(32),
+                    np.full(len(rows), offset & 0xFFFFFFFF, np.uint64),
+                    np.full(len(rows), (offset >> 32) & 0xFFFFFFFF, np.uint64)], axis=1)
+    r = po._philox(ctr, (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF))
+    u1 = ((r[:, 0] >> np.uint64(8)) + np.uint64(1)).astype(np.float64) * 2.0 ** -24
+    u2 = (r[:, 1] >> np.uint64(8)).astype(np.float64) * 2.0 ** -24
+    rad = np.sqrt(-2.0 * np.log(u1))
+    return np.stack([rad * np.cos(2 * math.pi * u2), rad * np.sin(2 * math.pi * u2)], axis=1)
+
+
+def test_full_size_policy_rollout_sampled(pkg, venv):
+    """BASELINE config 2 (65,536 formations x 10 agents) through the fused PPO collection kernel
+    (fenv_policy_rollout: policy + Gaussian sample + clip + env step x 10, last value, GAE), a
+    sample of formations checked against the CPU oracles: the policy against
+    oracle/policy_oracle.py (tolerance 2e-5 + 2e-5|ref|, as tests/test_gpu_policy.py), the noise
+    against its Philox restatement, every env transition bit for bit against the C oracle, GAE
+    against SB3's recurrence."""
+    from importlib import import_module
+
+    import policy_oracle as po
+    ro = import_module(pkg.__name__ + ".rollout")
+    pol_mod = import_module(pkg.__name__ + ".policy")
+    F, N, D = 65536, 10, 8
+    A = F * N
+    env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                             "goal_in_obs": True}, device=DEV, seed=3, reset_mode="philox")
+    pol = pol_mod.MlpPolicy(D, device=DEV, seed=2)
+    with torch.no_grad():  # non-trivial heads so the actions move the agents
+        pol.flat.add_(torch.randn(pol.flat.shape, generator=torch.Generator().manual_seed(5))
+                      .to(DEV) * 0.05)
+    buf = ro.RolloutBuffer(T, A, D, DEV)
+    col = ro.RolloutCollector(env, pol, buf, seed=11, fused=True)
+    col.collect()  # first rollout: states leave the reset distribution
+    pre = [v.cpu().numpy() for v in env.get_state()]
+    obs0 = col.last_obs.cpu().numpy()
+    off0 = col.offset
+    col.collect()
+    torch.cuda.synchronize()
+
+    rng = np.random.default_rng(17)
+    fs = np.unique(np.concatenate([rng.choice(F, 2000, replace=False), [0, 1, F - 2, F - 1]]))
+    ag = (fs[:, None] * N + np.arange(N)).reshape(-1)
+    agt = torch.from_numpy(ag).to(DEV)
+    S = len(ag)
+    get = lambda t: t[:, agt].cpu()  # noqa: E731
+    obs, mu, val = get(buf.observations), get(buf.mu), get(buf.values)
+    act, clp, lp = get(buf.actions), get(buf.clipped), get(buf.log_probs)
+    rew, dn, starts = get(buf.rewards), get(buf.dones), get(buf.episode_starts)
+    adv, ret = get(buf.advantages), get(buf.returns)
+    last_obs, last_val = col.last_obs[agt].cpu(), col._last_values[agt].cpu()
+    assert np.array_equal(bits(obs[0].numpy()), bits(obs0[ag]))
+
+    sd = po.unflatten(pol.flat.detach().cpu(), D)
+    mu_ref, v_ref = po.forward(sd, obs.reshape(-1, D))
+    torch.testing.assert_close(mu.reshape(-1, 2), mu_ref, atol=2e-5, rtol=2e-5)
+    torch.testing.assert_close(val.reshape(-1), v_ref, atol=2e-5, rtol=2e-5)
+    std = sd["log_std"].exp()
+    for j in range(T):
+        eps = torch.from_numpy(_normals(ag, 11, off0 + j)).float()
+        torch.testing.assert_close(act[j], mu[j] + std * eps, atol=5e-5, rtol=5e-5)
+    assert torch.equal(clp, act.clamp(-1, 1))
+    torch.testing.assert_close(lp.reshape(-1), po.log_prob(sd, mu.reshape(-1, 2),
+                                                           act.reshape(-1, 2)),
+                               atol=1e-4, rtol=1e-5)
+    _, lv_ref = po.forward(sd, last_obs)
+    torch.testing.assert_close(last_val, lv_ref, atol=2e-5, rtol=2e-5)
+
+    ref = COracleEnv(len(fs), N, True, 0)
+    ref.set_state(pre[0][ag], pre[1][ag], pre[2][fs], pre[3][fs], pre[4][fs])
+    for j in range(T):
+        o, r, d, _ = ref.step(np.ascontiguousarray(clp[j].numpy()))
+        nxt = obs[j + 1] if j + 1 < T else last_obs
+        assert np.array_equal(bits(nxt.numpy()), bits(o)), f"obs step {j}"
+        assert np.array_equal(bits(rew[j].numpy()), bits(r)), f"reward step {j}"
+        assert np.array_equal(dn[j].numpy(), d), f"done step {j}"
+
+    # GAE (SB3 RolloutBuffer.compute_returns_and_advantage), float64 recurrence
+    g, lam = buf.gamma, buf.gae_lambda
+    v64, r64 = val.double().numpy(), rew.double().numpy()
+    nt = 1.0 - np.concatenate([starts[1:].numpy(), dn[-1:].numpy()]).astype(np.float64)
+    nv = np.concatenate([v64[1:], last_val.double().numpy()[None]])
+    gae = np.zeros(S)
+    adv_ref = np.zeros((T, S))
+    for j in reversed(range(T)):
+        delta = r64[j] + g * nv[j] * nt[j] - v64[j]
+        gae = delta + g * lam * nt[j] * gae
+        adv_ref[j] = gae
+    np.testing.assert_allclose(adv.numpy(), adv_ref, rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(ret.numpy(), adv_ref + v64, rtol=1e-5, atol=1e-4)
