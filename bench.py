@@ -147,6 +147,41 @@ def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: 
             "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def random_action_bench(pkgname: str, dev, formations: int, agents: int, launches: int = 200,
+                        T: int = 10) -> dict:
+    """Secondary line: the north star's "synthetic random-action rollouts" with the actions drawn
+    inside the kernel (fenv_rollout_random, Philox) instead of read from HBM -- same env work,
+    8 B/agent-step less traffic.  Algorithmic bytes exclude the action read."""
+    import torch
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode="philox")
+    A = env.num_envs
+    obs = torch.empty((T, A, 8), device=dev)
+    rew = torch.empty((T, A), device=dev)
+    done = torch.empty((T, A), dtype=torch.bool, device=dev)
+    env.reset_tensor()
+    for k in range(3):
+        env.rollout_random(T, 7, k * T, obs, rew, done)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record()
+    for k in range(launches):
+        env.rollout_random(T, 7, (k + 3) * T, obs, rew, done)
+    b.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = a.elapsed_time(b) / launches
+    byts = rollout_bytes_per_launch(A, agents, 8, T) - 8.0 * A * T
+    return {"workload": f"{formations} formations x {agents} agents, fused {T}-step rollouts, "
+                        f"in-kernel Philox U(-1,1) actions",
+            "value": A * T * launches / el, "unit": "agent-steps/s", "avg_kernel_ms": ms,
+            "algorithmic_bytes_per_launch": byts,
+            "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
                      updates: int = 2) -> dict:
     """Secondary measurement: SB3's PPO.train at the reference's training config
@@ -357,6 +392,8 @@ def main():
         if world == 1 and not args.no_policy:
             out["ppo_update"] = ppo_update_bench(pkg.__name__, dev)
         if world == 1 and not args.no_configs:
+            out["random_action_rollout"] = random_action_bench(pkg.__name__, dev,
+                                                               args.formations, N)
             out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
                                   "config4": env_config_bench(pkg.__name__, dev, 16384, 64)}
         if world == 1 and not args.no_cpu_baseline:

@@ -86,6 +86,18 @@ int fenv_step(fenv_t *env, const float *act, float *obs, float *rew, uint8_t *do
 int fenv_rollout(fenv_t *env, int32_t T, const float *act, float *obs, float *rew,
                  uint8_t *done, float *partial, void *stream);
 
+/* Synthetic random-action rollout ("act_seed | act"; the north star's
+ * "synthetic random-action rollouts"): as fenv_rollout, but the actions are drawn inside the
+ * kernel instead of read from HBM.  Component c of agent a's action at step k is
+ * (w >> 8) / 2^23 - 1, exactly, in [-1, 1), with w = word (2 (s & 1) + c) of
+ * Philox4x32-10(counter = (g, s >> 1), key = act_seed), s = step_offset + k the global step
+ * index and g = the global agent index (first_formation * N + a: shard-invariant).  act_out
+ * (may be NULL) receives the actions [T][A][2]; feeding them to fenv_rollout from the same state
+ * gives bit-identical results. */
+int fenv_rollout_random(fenv_t *env, int32_t T, uint64_t act_seed, uint64_t step_offset,
+                        float *act_out, float *obs, float *rew, uint8_t *done, float *partial,
+                        void *stream);
+
 /* Number of float2 partial records fenv_rollout writes (one per workgroup). */
 int64_t fenv_partial_count(const fenv_t *env);
 

@@ -38,6 +38,7 @@ SIGNATURES = {
     "fenv_observe": (_I32, [_P, _P, _P]),
     "fenv_step": (_I32, [_P, _P, _P, _P, _P, _P]),
     "fenv_rollout": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
+    "fenv_rollout_random": (_I32, [_P, _I32, _U64, _U64, _P, _P, _P, _P, _P, _P]),
     "fenv_partial_count": (_I64, [_P]),
     "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
     "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),

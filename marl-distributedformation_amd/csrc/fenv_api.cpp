@@ -238,11 +238,10 @@ int fenv_observe(fenv_t *e, float *obs, void *stream) {
     return FENV_OK;
 }
 
-int fenv_rollout(fenv_t *e, int32_t T, const float *act, float *obs, float *rew, uint8_t *done,
-                 float *partial, void *stream) {
-    if (!e) return fail(FENV_EINVAL, "fenv_rollout: NULL handle");
-    if (T < 0) return fail(FENV_EINVAL, "fenv_rollout: T must be >= 0");
-    if (!act && T > 0) return fail(FENV_EINVAL, "fenv_rollout: act is NULL");
+// fenv_rollout / fenv_rollout_random: T fused steps, split at MT19937 reset events.  gen = NULL:
+// actions from `act`; else generated in the kernel (gen->offset / gen->out advance per launch).
+static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::ActGen *gen,
+                        float *obs, float *rew, uint8_t *done, float *partial, void *stream) {
     FENV_HIP(hipSetDevice(e->device));
     hipStream_t st = as_stream(stream);
     const int64_t A = e->A, D = e->D;
@@ -260,10 +259,16 @@ int fenv_rollout(fenv_t *e, int32_t T, const float *act, float *obs, float *rew,
                 event = true;
             }
         }
+        fenvk::ActGen g{};
+        if (gen) {
+            g = *gen;
+            g.offset += (uint64_t)k0;
+            if (g.out) g.out += k0 * A * 2;
+        }
         FENV_HIP(fenvk::launch_rollout(
-            e->c, e->s, e->pending(), (int32_t)L, (int32_t)D, act + k0 * A * 2,
+            e->c, e->s, e->pending(), (int32_t)L, (int32_t)D, act ? act + k0 * A * 2 : nullptr,
             obs ? obs + k0 * A * D : nullptr, rew ? rew + k0 * A : nullptr,
-            done ? done + k0 * A : nullptr, partial, k0 > 0, st));
+            done ? done + k0 * A : nullptr, partial, k0 > 0, st, gen ? &g : nullptr));
         e->advance_t(L);
         if (event) {
             int rc = e->gen_pending(st);
@@ -272,6 +277,27 @@ int fenv_rollout(fenv_t *e, int32_t T, const float *act, float *obs, float *rew,
         k0 += L;
     }
     return FENV_OK;
+}
+
+int fenv_rollout(fenv_t *e, int32_t T, const float *act, float *obs, float *rew, uint8_t *done,
+                 float *partial, void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_rollout: NULL handle");
+    if (T < 0) return fail(FENV_EINVAL, "fenv_rollout: T must be >= 0");
+    if (!act && T > 0) return fail(FENV_EINVAL, "fenv_rollout: act is NULL");
+    return rollout_impl(e, T, act, nullptr, obs, rew, done, partial, stream);
+}
+
+int fenv_rollout_random(fenv_t *e, int32_t T, uint64_t act_seed, uint64_t step_offset,
+                        float *act_out, float *obs, float *rew, uint8_t *done, float *partial,
+                        void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_rollout_random: NULL handle");
+    if (T < 0) return fail(FENV_EINVAL, "fenv_rollout_random: T must be >= 0");
+    fenvk::ActGen g{};
+    g.k0 = (uint32_t)act_seed;
+    g.k1 = (uint32_t)(act_seed >> 32);
+    g.offset = step_offset;
+    g.out = act_out;
+    return rollout_impl(e, T, nullptr, &g, obs, rew, done, partial, stream);
 }
 
 int fenv_step(fenv_t *e, const float *act, float *obs, float *rew, uint8_t *done, void *stream) {

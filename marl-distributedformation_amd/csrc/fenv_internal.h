@@ -42,9 +42,18 @@ int64_t group_count(const Consts &c);  // 4-wave workgroups (N<=64) or formation
 // workgroups of the rollout/step launch = records of its stats partials
 int64_t rollout_group_count(const Consts &c);
 
+// In-kernel synthetic actions (fenv_rollout_random): U(-1, 1) per component from Philox4x32-10
+// keyed by act_seed, counter (global agent, global step / 2); one call serves two steps.
+struct ActGen {
+    uint32_t k0, k1;  // Philox key = act_seed
+    uint64_t offset;  // global step index of the launch's local step 0
+    float *out;       // optional [T][A][2] copy of the actions (NULL: not written)
+};
+
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
-                          float *partial, bool accumulate, hipStream_t st);
+                          float *partial, bool accumulate, hipStream_t st,
+                          const ActGen *gen = nullptr);
 hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPending &p,
                                 int32_t D, bool do_reset, float *obs, hipStream_t st);
 hipError_t launch_metrics(const Consts &c, const DevState &s, const float *rew, float *out,

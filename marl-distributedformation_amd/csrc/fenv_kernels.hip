@@ -21,12 +21,17 @@
 namespace fenvk {
 
 // ---------------------------------------------------------------- fused T-step rollout
-template <int D, int MODE, class X>
+// Synthetic action component in [-1, 1) from 24 random bits, exactly: (w >> 8) / 2^23 - 1.
+__device__ __forceinline__ float act_u24(uint32_t w) {
+    return (float)((int32_t)(w >> 8) - (1 << 23)) * 0x1.0p-23f;
+}
+
+template <int D, int MODE, bool RA, class X>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
                                              int M, int64_t a_first, int32_t T,
-                                             const float2 *__restrict__ act,
+                                             const float2 *__restrict__ act, const ActGen &gen,
                                              float *__restrict__ obs, float *__restrict__ rew,
                                              uint8_t *__restrict__ done, float &rsum,
                                              float &dsum) {
@@ -46,18 +51,32 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
 #ifndef FENV_ACT_PREFETCH
 #define FENV_ACT_PREFETCH 1
 #endif
-    constexpr int kPF = FENV_ACT_PREFETCH;
+    constexpr int kPF = RA ? 1 : FENV_ACT_PREFETCH;
     float2 ring[kPF];
+    const int64_t ga = c.f0 * c.N + a;  // global agent index (shard-invariant actions)
+    uint4 words = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int j = 0; j < kPF; ++j)
-        ring[j] = (active && j < T) ? act[(int64_t)j * A + a] : make_float2(0.f, 0.f);
+        ring[j] = (!RA && active && j < T) ? act[(int64_t)j * A + a] : make_float2(0.f, 0.f);
     for (int32_t k0 = 0; k0 < T; k0 += kPF) {
 #pragma unroll
         for (int j = 0; j < kPF; ++j) {
             const int32_t k = k0 + j;
             if (k >= T) break;
-            const float2 ac = ring[j];
-            if (active && k + kPF < T) ring[j] = act[(int64_t)(k + kPF) * A + a];
+            float2 ac = ring[j];
+            if (RA) {
+                const uint64_t gs = gen.offset + (uint64_t)k;
+                if (k == 0 || (gs & 1) == 0)
+                    words = philox(make_uint4((uint32_t)ga, (uint32_t)((uint64_t)ga >> 32),
+                                              (uint32_t)(gs >> 1), (uint32_t)(gs >> 33)),
+                                   gen.k0, gen.k1);
+                ac = (gs & 1) ? make_float2(act_u24(words.z), act_u24(words.w))
+                              : make_float2(act_u24(words.x), act_u24(words.y));
+                if (gen.out && active)
+                    reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
+            } else if (active && k + kPF < T) {
+                ring[j] = act[(int64_t)(k + kPF) * A + a];
+            }
             float rw;
             bool dn, rs;
             env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
@@ -88,9 +107,10 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
     }
 }
 
-template <int D, int MODE>
+template <int D, int MODE, bool RA>
 __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, DevPending p,
                                                       int32_t T, const float2 *__restrict__ act,
+                                                      ActGen gen,
                                                       float *__restrict__ obs,
                                                       float *__restrict__ rew,
                                                       uint8_t *__restrict__ done,
@@ -114,8 +134,8 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
     const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
     float rsum = 0.f, dsum = 0.f;
     if (M > 0)
-        rollout_body<D, MODE>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N, T,
-                              act, obs, rew, done, rsum, dsum);
+        rollout_body<D, MODE, RA>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
+                                  T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -131,10 +151,11 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
     }
 }
 
-template <int D, int MODE>
+template <int D, int MODE, bool RA>
 __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, DevPending p,
                                                         int32_t T,
                                                         const float2 *__restrict__ act,
+                                                        ActGen gen,
                                                         float *__restrict__ obs,
                                                         float *__restrict__ rew,
                                                         uint8_t *__restrict__ done,
@@ -152,8 +173,8 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     const int w = i >> 6;
     const int M = N - 64 * w < 64 ? (N - 64 * w > 0 ? N - 64 * w : 0) : 64;
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE>(c, st, p, x, active, f, a, i, stage[w], i & 63, M, f * N + 64 * w, T,
-                          act, obs, rew, done, rsum, dsum);
+    rollout_body<D, MODE, RA>(c, st, p, x, active, f, a, i, stage[w], i & 63, M, f * N + 64 * w,
+                              T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -569,33 +590,49 @@ static inline unsigned block_threads(int32_t N) { return (unsigned)((N + 63) / 6
 template <int D, int MODE>
 static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                              const float *act, float *obs, float *rew, uint8_t *done,
-                             float *partial, bool accum, hipStream_t st) {
+                             float *partial, bool accum, hipStream_t st, const ActGen *gen) {
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
+    if (gen) {  // in-kernel actions
+        if (wave_path(c.N))
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, true>), dim3((unsigned)group_count(c)),
+                               dim3(256), 0, st, c, s, p, T, a2, *gen, obs, rew, done, p2, accum);
+        else
+            hipLaunchKernelGGL((k_rollout_block<D, MODE, true>), dim3((unsigned)c.F),
+                               dim3(block_threads(c.N)), 0, st, c, s, p, T, a2, *gen, obs, rew,
+                               done, p2, accum);
+        return hipGetLastError();
+    }
+    const ActGen g0{};
     if (FENV_RW && wave_path(c.N)) {
         hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
                            dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
                            accum);
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
-        hipLaunchKernelGGL((k_rollout_wave<D, MODE>), dim3(blocks), dim3(256), 0, st, c, s, p, T,
-                           a2, obs, rew, done, p2, accum);
+        hipLaunchKernelGGL((k_rollout_wave<D, MODE, false>), dim3(blocks), dim3(256), 0, st, c, s,
+                           p, T, a2, g0, obs, rew, done, p2, accum);
     } else {
-        hipLaunchKernelGGL((k_rollout_block<D, MODE>), dim3((unsigned)c.F), dim3(block_threads(c.N)),
-                           0, st, c, s, p, T, a2, obs, rew, done, p2, accum);
+        hipLaunchKernelGGL((k_rollout_block<D, MODE, false>), dim3((unsigned)c.F),
+                           dim3(block_threads(c.N)), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2,
+                           accum);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
-                          float *partial, bool accum, hipStream_t st) {
+                          float *partial, bool accum, hipStream_t st, const ActGen *gen) {
     const bool mt = c.reset_mode == FENV_RESET_MT19937;
     if (D == 8)
-        return mt ? rollout_dm<8, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial, accum, st)
-                  : rollout_dm<8, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial, accum, st);
-    return mt ? rollout_dm<6, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial, accum, st)
-              : rollout_dm<6, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial, accum, st);
+        return mt ? rollout_dm<8, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial,
+                                                      accum, st, gen)
+                  : rollout_dm<8, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial,
+                                                     accum, st, gen);
+    return mt ? rollout_dm<6, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial, accum,
+                                                  st, gen)
+              : rollout_dm<6, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial, accum,
+                                                 st, gen);
 }
 
 template <int D, int MODE, bool RESET>

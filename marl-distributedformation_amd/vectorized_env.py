@@ -313,6 +313,31 @@ class FormationEnv:
                                            self._stream()), "fenv_rollout")
         return obs, rew, done
 
+    def rollout_random(self, T: int, act_seed: int = 0, step_offset: int = 0, obs=None,
+                       rew=None, done=None, partial=None, act_out=None):
+        """Synthetic random-action rollout (``fenv_rollout_random``): T fused env steps whose
+        U(-1, 1) actions are drawn inside the kernel from Philox keyed by ``act_seed``, counter
+        (global agent, (step_offset + k) // 2).  ``act_out`` [T, A, 2] (optional) receives the
+        actions; :meth:`rollout` on them from the same state returns the same bits."""
+        T = int(T)
+        if T < 0:
+            raise ValueError("T must be >= 0")
+        A, D, dev = self.num_envs, self.obs_dim, self.device
+        if obs is None:
+            obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
+        if rew is None:
+            rew = torch.empty((T, A), dtype=torch.float32, device=dev)
+        if done is None:
+            done = torch.empty((T, A), dtype=torch.bool, device=dev)
+        if act_out is not None and (tuple(act_out.shape) != (T, A, 2) or
+                                    act_out.dtype != torch.float32 or act_out.device != dev):
+            raise ValueError(f"act_out must be float32 [{T}, {A}, 2] on {dev}")
+        _lib.check(_lib.lib().fenv_rollout_random(
+            self._h, T, int(act_seed) & 0xFFFFFFFFFFFFFFFF, int(step_offset) & 0xFFFFFFFFFFFFFFFF,
+            _lib.ptr(act_out), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done), _lib.ptr(partial),
+            self._stream()), "fenv_rollout_random")
+        return obs, rew, done
+
     def policy_rollout(self, params: torch.Tensor, T: int, bufs: dict, seed: int = 0,
                        offset: int = 0, deterministic: bool = False, gamma: float = 0.99,
                        gae_lambda: float = 0.95) -> None:

@@ -53,6 +53,24 @@ def synth_actions(seed: int, step: int, num_agents: int, amp: float = 1.0) -> np
     return a.astype(np.float32).reshape(num_agents, 2)
 
 
+def philox_actions(act_seed: int, step: int, first_agent: int, num_agents: int) -> np.ndarray:
+    """The actions fenv_rollout_random draws in the kernel (include/fenv.h) for global step
+    `step` and global agents [first_agent, first_agent + num_agents): component c is
+    (w >> 8) / 2^23 - 1 with w = word 2 (step & 1) + c of Philox4x32-10(counter = (agent,
+    step >> 1), key = act_seed).  Not a reference behaviour (the reference takes actions from its
+    caller); the build's own synthetic-action generator, restated to check the kernel."""
+    from policy_oracle import _philox
+    g = np.arange(first_agent, first_agent + num_agents, dtype=np.uint64)
+    pair = np.uint64(step >> 1)
+    M = np.uint64(0xFFFFFFFF)
+    ctr = np.stack([g & M, g >> np.uint64(32), np.full_like(g, pair & M),
+                    np.full_like(g, pair >> np.uint64(32))], axis=1)
+    w = _philox(ctr, (act_seed & 0xFFFFFFFF, (act_seed >> 32) & 0xFFFFFFFF))
+    w = w[:, 2:4] if step & 1 else w[:, 0:2]
+    v = (w >> np.uint64(8)).astype(np.int64) - (1 << 23)
+    return (v.astype(np.float32) * np.float32(2.0 ** -23)).astype(np.float32)
+
+
 # ----------------------------------------------------------------------------- MT19937
 def mt_raw(seed: int, n: int, skip: int = 0) -> np.ndarray:
     """Raw 32-bit MT19937 outputs after init_genrand(seed) (== torch.manual_seed stream)."""

@@ -318,3 +318,48 @@ def test_visualize_mirror(venv):
     env.step(np.full((5, 2), 0.5, np.float32))
     px, py, _, _, _ = (v.cpu().numpy() for v in env.get_state())
     assert tuple(env._fig.dots[0].center) == (float(px[0]), float(py[0]))
+
+
+@pytest.mark.parametrize("N,mode,T,offset", [(5, "philox", 10, 0), (10, "philox", 7, 3),
+                                              (64, "mt19937", 13, 5), (100, "mt19937", 6, 1),
+                                              (7, "mt19937", 25, 2)])
+def test_rollout_random_actions(venv, N, mode, T, offset):
+    """fenv_rollout_random: the in-kernel actions are oracle.philox_actions bit for bit (also
+    for a shard), and the rollout equals fenv_rollout fed with those actions from the same state
+    -- across MT19937 reset events (max_steps 9) that split the launch."""
+    from oracle import philox_actions
+    F, seed = 40, 77
+    envs = [make_env(venv, F, N, True, 3, reset_mode=mode, max_steps=9) for _ in range(2)]
+    for e in envs:
+        e.reset_tensor()
+    A = F * N
+    act = torch.empty((T, A, 2), dtype=torch.float32, device=DEV)
+    part = torch.zeros((envs[0].partial_count(), 2), dtype=torch.float32, device=DEV)
+    o1, r1, d1 = envs[0].rollout_random(T, seed, offset, act_out=act, partial=part)
+    o2, r2, d2 = envs[1].rollout(act)
+    torch.cuda.synchronize()
+    a = act.cpu().numpy()
+    for k in range(T):
+        assert np.array_equal(bits(a[k]), bits(philox_actions(seed, offset + k, 0, A))), k
+    assert a.min() >= -1.0 and a.max() < 1.0
+    assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2)
+    if T > 11:
+        assert bool(d1.any())  # a reset event inside the launch
+    for s1, s2 in zip(envs[0].get_state(), envs[1].get_state()):
+        assert torch.equal(s1, s2)
+    assert abs(envs[0].reduce_partials(part)[0].item() - r1.double().sum().item()) <= \
+        1e-5 * abs(r1.double().sum().item())
+    # shard invariance: formations [10, 30) of a 60-formation env draw the same actions
+    sh = venv.FormationEnv({"num_formation": 20, "num_agents_per_formation": N,
+                            "goal_in_obs": True}, device=DEV, seed=3, reset_mode="philox",
+                           first_formation=10, total_formations=60)
+    sh.reset_tensor()
+    a2 = torch.empty((2, 20 * N, 2), dtype=torch.float32, device=DEV)
+    sh.rollout_random(2, seed, offset, act_out=a2, obs=None)
+    assert np.array_equal(bits(a2[1].cpu().numpy()),
+                          bits(philox_actions(seed, offset + 1, 10 * N, 20 * N)))
+    # without act_out nothing else changes
+    envs[1].set_state(*envs[0].get_state())
+    o3, r3, d3 = envs[0].rollout_random(3, seed, offset + T)
+    o4, r4, d4 = envs[1].rollout_random(3, seed, offset + T, act_out=torch.empty_like(act[:3]))
+    assert torch.equal(o3, o4) and torch.equal(r3, r4) and torch.equal(d3, d4)
