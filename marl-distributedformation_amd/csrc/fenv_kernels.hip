@@ -26,7 +26,69 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
     return (float)((int32_t)(w >> 8) - (1 << 23)) * 0x1.0p-23f;
 }
 
-template <int D, int MODE, bool RA, class X>
+// Workgroup-staged reward/done rows (k_rollout_wave_rs): the kRS waves of a workgroup cover one
+// contiguous agent slice (8 x 60 = 480 agents at N = 5: a 1,920-B reward row = 15 whole 128-B
+// lines, where a wave's own 240-B row straddles lines shared with its neighbours).  Rewards and
+// dones of kRSTB steps are buffered in LDS and written as whole slice rows after one barrier;
+// observations and actions stay per wave (their rows are already 128-B-line multiples).
+#ifndef FENV_RS
+#define FENV_RS 1  // 0: k_rollout_wave with per-wave reward/done stores
+#endif
+#ifndef FENV_RS_TB
+#define FENV_RS_TB 8
+#endif
+// Register budget: left to the compiler (79 VGPRs -> 6 waves/SIMD, 3 workgroups per CU).  Forcing
+// 64 VGPRs (4 workgroups per CU) spills and runs ~12 % slower (tools/env_ab.sh).
+#ifndef FENV_RS_OCC
+#define FENV_RS_OCC
+#endif
+constexpr int kRS = 8;
+constexpr int kRSA = 64 * kRS;
+constexpr int kRSTB = FENV_RS_TB;
+
+struct RSStage {
+    float *rbuf;    // [kRSTB][kRSA]
+    uint8_t *dbuf;  // [kRSTB][kRSA]
+    int li;         // this lane's slot in the slice (w * agents-per-wave + lane)
+    int nwg;        // agents in the slice
+    int64_t g0;     // first agent of the slice
+};
+
+// rows [kfirst, kfirst + nrows) of the slice from the LDS buffers (all kRSA threads).  Vector
+// path: thread (c4 = tid & 127, tid >> 7) stores 16 B of reward / 4 B of done per row, 4 rows per
+// pass (a slice has at most kRSA = 512 agents = 128 float4).
+__device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows, int64_t A,
+                                         float *__restrict__ rew, uint8_t *__restrict__ done) {
+    const int tid = threadIdx.x, n = r.nwg;
+    const int c4 = tid & 127, r0 = tid >> 7;
+    const bool vec = ((n | (int)(A & 3)) & 3) == 0;
+    if (rew) {
+        float *base = rew + (int64_t)kfirst * A + r.g0;
+        if (vec && (reinterpret_cast<uintptr_t>(base) & 15) == 0) {
+            if (c4 < (n >> 2))
+                for (int row = r0; row < nrows; row += 4)
+                    reinterpret_cast<float4 *>(base + (int64_t)row * A)[c4] =
+                        reinterpret_cast<const float4 *>(r.rbuf + row * kRSA)[c4];
+        } else if (tid < n) {
+            for (int row = 0; row < nrows; ++row)
+                base[(int64_t)row * A + tid] = r.rbuf[row * kRSA + tid];
+        }
+    }
+    if (done) {
+        uint8_t *base = done + (int64_t)kfirst * A + r.g0;
+        if (vec && (reinterpret_cast<uintptr_t>(base) & 3) == 0) {
+            if (c4 < (n >> 2))
+                for (int row = r0; row < nrows; row += 4)
+                    reinterpret_cast<uint32_t *>(base + (int64_t)row * A)[c4] =
+                        reinterpret_cast<const uint32_t *>(r.dbuf + row * kRSA)[c4];
+        } else if (tid < n) {
+            for (int row = 0; row < nrows; ++row)
+                base[(int64_t)row * A + tid] = r.dbuf[row * kRSA + tid];
+        }
+    }
+}
+
+template <int D, int MODE, bool RA, bool RS, class X>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
@@ -34,7 +96,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
                                              const float2 *__restrict__ act, const ActGen &gen,
                                              float *__restrict__ obs, float *__restrict__ rew,
                                              uint8_t *__restrict__ done, float &rsum,
-                                             float &dsum) {
+                                             float &dsum, const RSStage &rsg = RSStage{}) {
     const int64_t A = c.F * (int64_t)c.N;
     Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
     if (active) {
@@ -58,38 +120,60 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
 #pragma unroll
     for (int j = 0; j < kPF; ++j)
         ring[j] = (!RA && active && j < T) ? act[(int64_t)j * A + a] : make_float2(0.f, 0.f);
-    for (int32_t k0 = 0; k0 < T; k0 += kPF) {
-#pragma unroll
-        for (int j = 0; j < kPF; ++j) {
-            const int32_t k = k0 + j;
-            if (k >= T) break;
-            float2 ac = ring[j];
-            if (RA) {
-                const uint64_t gs = gen.offset + (uint64_t)k;
-                if (k == 0 || (gs & 1) == 0)
-                    words = philox(make_uint4((uint32_t)ga, (uint32_t)((uint64_t)ga >> 32),
-                                              (uint32_t)(gs >> 1), (uint32_t)(gs >> 33)),
-                                   gen.k0, gen.k1);
-                ac = (gs & 1) ? make_float2(act_u24(words.z), act_u24(words.w))
-                              : make_float2(act_u24(words.x), act_u24(words.y));
-                if (gen.out && active)
-                    reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
-            } else if (active && k + kPF < T) {
-                ring[j] = act[(int64_t)(k + kPF) * A + a];
-            }
-            float rw;
-            bool dn, rs;
-            env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
-            any_reset |= rs;
-            const int64_t row = (int64_t)k * A + a;
-            float o[8];
-            env_obs<D>(x, s, o);
-            if (obs) store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-            if (active) {
+    // one env step k with action slot j of the prefetch ring
+    auto step = [&](int32_t k, int j) {
+        float2 ac = ring[j];
+        if (RA) {
+            const uint64_t gs = gen.offset + (uint64_t)k;
+            if (k == 0 || (gs & 1) == 0)
+                words = philox(make_uint4((uint32_t)ga, (uint32_t)((uint64_t)ga >> 32),
+                                          (uint32_t)(gs >> 1), (uint32_t)(gs >> 33)),
+                               gen.k0, gen.k1);
+            ac = (gs & 1) ? make_float2(act_u24(words.z), act_u24(words.w))
+                          : make_float2(act_u24(words.x), act_u24(words.y));
+            if (gen.out && active) reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
+        } else if (active && k + kPF < T) {
+            ring[j] = act[(int64_t)(k + kPF) * A + a];
+        }
+        float rw;
+        bool dn, rs;
+        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        any_reset |= rs;
+        const int64_t row = (int64_t)k * A + a;
+        float o[8];
+        env_obs<D>(x, s, o);
+        if (obs) store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
+        if (active) {
+            if (RS) {
+                const int kb = k % kRSTB;
+                rsg.rbuf[kb * kRSA + rsg.li] = rw;
+                rsg.dbuf[kb * kRSA + rsg.li] = (uint8_t)dn;
+            } else {
                 if (rew) rew[row] = rw;
                 if (done) done[row] = (uint8_t)dn;
-                rsum += rw;
-                dsum += dn ? 1.0f : 0.0f;
+            }
+            rsum += rw;
+            dsum += dn ? 1.0f : 0.0f;
+        }
+    };
+    if (RS) {  // chunks of kRSTB steps, each followed by one workgroup flush of its rows
+        static_assert(!RS || kPF == 1, "staged rows use the one-step prefetch");
+#pragma unroll 1
+        for (int32_t kc = 0; kc < T; kc += kRSTB) {
+            const int32_t ke = T - kc < kRSTB ? T : kc + kRSTB;
+#pragma unroll 1
+            for (int32_t k = kc; k < ke; ++k) step(k, 0);
+            __syncthreads();
+            rs_flush(rsg, kc, ke - kc, A, rew, done);
+            if (ke < T) __syncthreads();
+        }
+    } else {
+        for (int32_t k0 = 0; k0 < T; k0 += kPF) {
+#pragma unroll
+            for (int j = 0; j < kPF; ++j) {
+                const int32_t k = k0 + j;
+                if (k >= T) break;
+                step(k, j);
             }
         }
     }
@@ -134,8 +218,8 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
     const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
     float rsum = 0.f, dsum = 0.f;
     if (M > 0)
-        rollout_body<D, MODE, RA>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
-                                  T, act, gen, obs, rew, done, rsum, dsum);
+        rollout_body<D, MODE, RA, false>(c, st, p, x, active, f, a, i, stage[w], lane, M,
+                                         f_first * N, T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -145,6 +229,58 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
             float2 v = red[0];
             for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
                 v = make_float2(v.x + red[k].x, v.y + red[k].y);
+            if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
+            partial[blockIdx.x] = v;
+        }
+    }
+}
+
+template <int D, int MODE, bool RA>
+__global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, DevState st, DevPending p,
+                                                          int32_t T,
+                                                          const float2 *__restrict__ act,
+                                                          ActGen gen, float *__restrict__ obs,
+                                                          float *__restrict__ rew,
+                                                          uint8_t *__restrict__ done,
+                                                          float2 *__restrict__ partial,
+                                                          bool accum) {
+    // Every wave runs the step loop (the flushes are workgroup barriers); waves past the last
+    // formation have no active lane and write nothing.
+    __shared__ __attribute__((aligned(16))) float stage[kRS][64 * 8];
+    __shared__ __attribute__((aligned(16))) float rbuf[kRSTB * kRSA];
+    __shared__ __attribute__((aligned(16))) uint8_t dbuf[kRSTB * kRSA];
+    __shared__ float2 red[kRS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * kRS + w;
+    const int N = c.N;
+    const int Mw = c.fpw * N;  // agents of a full wave
+    const int fi = lane / N;
+    const int i = lane - fi * N;
+    const int64_t f = wave * c.fpw + fi;
+    const bool active = fi < c.fpw && f < c.F;
+    const int64_t a = f * N + i;
+    WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
+    const int64_t f_first = wave * c.fpw;
+    const int64_t f_left = c.F - f_first;
+    const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
+    const int64_t A = c.F * (int64_t)N;
+    RSStage rsg;
+    rsg.rbuf = rbuf;
+    rsg.dbuf = dbuf;
+    rsg.li = w * Mw + lane;
+    rsg.g0 = (int64_t)blockIdx.x * kRS * Mw;
+    rsg.nwg = (int)((A - rsg.g0) < (int64_t)kRS * Mw ? (A - rsg.g0) : (int64_t)kRS * Mw);
+    float rsum = 0.f, dsum = 0.f;
+    rollout_body<D, MODE, RA, true>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
+                                    T, act, gen, obs, rew, done, rsum, dsum, rsg);
+    if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
+        rsum = wave_sum(rsum);
+        dsum = wave_sum(dsum);
+        if (lane == 0) red[w] = make_float2(rsum, dsum);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float2 v = red[0];
+            for (int k = 1; k < kRS; ++k) v = make_float2(v.x + red[k].x, v.y + red[k].y);
             if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
             partial[blockIdx.x] = v;
         }
@@ -173,8 +309,8 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     const int w = i >> 6;
     const int M = N - 64 * w < 64 ? (N - 64 * w > 0 ? N - 64 * w : 0) : 64;
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA>(c, st, p, x, active, f, a, i, stage[w], i & 63, M, f * N + 64 * w,
-                              T, act, gen, obs, rew, done, rsum, dsum);
+    rollout_body<D, MODE, RA, false>(c, st, p, x, active, f, a, i, stage[w], i & 63, M,
+                                     f * N + 64 * w, T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -582,6 +718,7 @@ int64_t group_count(const Consts &c) {
 
 int64_t rollout_group_count(const Consts &c) {
     if (FENV_RW && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
+    if (FENV_RS && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRS - 1) / kRS;
     return group_count(c);
 }
 
@@ -594,7 +731,11 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
     if (gen) {  // in-kernel actions
-        if (wave_path(c.N))
+        if (FENV_RS && wave_path(c.N))
+            hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, true>),
+                               dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p,
+                               T, a2, *gen, obs, rew, done, p2, accum);
+        else if (wave_path(c.N))
             hipLaunchKernelGGL((k_rollout_wave<D, MODE, true>), dim3((unsigned)group_count(c)),
                                dim3(256), 0, st, c, s, p, T, a2, *gen, obs, rew, done, p2, accum);
         else
@@ -608,6 +749,10 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
         hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
                            dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
                            accum);
+    } else if (FENV_RS && wave_path(c.N)) {
+        hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
+                           dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p, T,
+                           a2, g0, obs, rew, done, p2, accum);
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
         hipLaunchKernelGGL((k_rollout_wave<D, MODE, false>), dim3(blocks), dim3(256), 0, st, c, s,
