@@ -40,29 +40,60 @@ def rollout_bytes_per_launch(A: int, N: int, D: int, T: int) -> float:
     return A * (T * per_step + per_launch)
 
 
-def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
-    """Time the bit-exact C port of the reference env (oracle/, 1 thread) on a bounded sample
-    of the same workload (random U(-1,1) actions, 5 agents/formation)."""
+def _cpu_oracle_rate(F: int, N: int, D: int, threads: int, budget_s: float):
+    """Step `threads` independent shards of F formations (one C oracle env per thread, ctypes
+    drops the GIL for the call) until `budget_s` has passed; returns (agent-steps/s, steps)."""
+    import threading
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import COracleEnv
-    F = 65536
-    env = COracleEnv(F, N, D == 8, 0)
-    env.reset()
-    rng = np.random.default_rng(0)
-    acts = [rng.uniform(-1, 1, (F * N, 2)).astype(np.float32) for _ in range(4)]
-    steps = 0
+    shards = [F // threads + (1 if t < F % threads else 0) for t in range(threads)]
+    envs = [COracleEnv(f, N, D == 8, t) for t, f in enumerate(shards)]
+    for e in envs:
+        e.reset()
+    acts = [[np.random.default_rng(t * 4 + k).uniform(-1, 1, (f * N, 2)).astype(np.float32)
+             for k in range(4)] for t, f in enumerate(shards)]
+    steps = [0] * threads
     t0 = time.perf_counter()
-    while True:
-        env.step_inplace(acts[steps % 4])
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": F * N * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{F} formations x {N} agents, {steps} env steps ({el:.1f} s), "
-                      f"oracle/fenv_oracle.c (bit-exact C port of simulate.py/vectorized_env.py)"
-                      f", 1 thread of {os.cpu_count()} host CPUs"}
+    deadline = t0 + budget_s
+
+    def run(t):
+        e, a, k = envs[t], acts[t], 0
+        while time.perf_counter() < deadline:
+            e.step_inplace(a[k % 4])
+            k += 1
+        steps[t] = k
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    return sum(f * N * k for f, k in zip(shards, steps)) / el, min(steps), el
+
+
+def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
+    """Time the bit-exact C port of the reference env (oracle/fenv_oracle.c) on a bounded
+    sample of the same workload (random U(-1,1) actions, 5 agents/formation): first 1 thread,
+    then one thread per host core of this job's CPU share (<= 16 on the GPU box) over
+    formation shards.  `value` is the multi-threaded rate; `cores` the threads used."""
+    F = 65536
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    threads = max(1, min(16, share))
+    one, one_steps, one_el = _cpu_oracle_rate(F, N, D, 1, budget_s / 2)
+    many, many_steps, many_el = _cpu_oracle_rate(F, N, D, threads, budget_s / 2)
+    return {"value": many, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "single_thread_value": one,
+            "sample": f"{F} formations x {N} agents: 1 thread {one_steps} env steps "
+                      f"({one_el:.1f} s), then {threads} threads over {threads} formation "
+                      f"shards >= {many_steps} env steps each ({many_el:.1f} s); "
+                      f"oracle/fenv_oracle.c (bit-exact C port of simulate.py/"
+                      f"vectorized_env.py); host reports {os.cpu_count()} CPUs, "
+                      f"affinity {share}"}
 
 
 def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollouts: int) -> dict:
