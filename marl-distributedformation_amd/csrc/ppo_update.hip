@@ -9,19 +9,23 @@
 // Why one workgroup: a minibatch step depends on the previous step's parameters, and a 64-sample
 // step of this 9,669-parameter MLP is ~1.8 MFLOP -- far too little to spread over the chip, and
 // ~100 tiny launches per step in torch (~430 us replayed as a HIP graph).  Here the parameters,
-// their gradients and the minibatch's activations live in LDS (151 KB), each thread keeps the
+// their gradients and the minibatch's activations live in LDS (152 KB), each thread keeps the
 // Adam moments of the ~19 parameters it owns in registers, and the loop runs every minibatch of
-// every epoch inside one launch.  The three 64-deep contractions are register-blocked 8 ways so a multiply-add costs
-// ~1 LDS read instead of 2.  All arithmetic is fp32 VALU (fmaf chains); results match the torch
-// path to summation-order rounding (tests/test_gpu_rollout.py).
+// every epoch inside one launch.  The 64-deep contractions (layer 2 forward, W2 gradients,
+// dL/dh1, W1 gradients) run on the fp32 MFMA pipe (v_mfma_f32_32x32x2f32 / 16x16x4f32: exact
+// fp32 products, fp32 accumulation); the parameter and gradient images are padded (lx) so the
+// operand reads are bank-conflict free.  Results match the torch path to summation-order
+// rounding (tests/test_gpu_rollout.py).
 //
-// Work split per minibatch (B <= 64 samples, 16 waves, lane = sample or = hidden unit):
-//   forward  layer 1/2: wave w computes hidden units 8w..8w+7 (of 2 x 64) for lane = sample;
-//            activation rows are padded to 65 floats so the 64 lanes hit 64 banks.
+// Work split per minibatch (B <= 64 samples, 8 waves, 2 per SIMD):
+//   forward  layer 1: lane = sample, 16 hidden units per wave (VALU, 8-deep);
+//            layer 2: wave w = one 32 x 32 tile (net, sample rows, hidden cols), 32 MFMAs.
+//            Activation rows are padded to 65 floats; all 64 rows run (rows >= B are unused).
 //   loss     wave 0, lane = sample: heads, log-prob, ratio, clipped surrogate, value loss, and the
 //            per-sample gradients w.r.t. mu, value, log_std (torch's min/clamp subgradients).
-//   backward head weights (lane = k), dL/dz2 in place of the layer-2 activations, W2/b2 grads
-//            (lane = k, wave-uniform row), dL/dz1 in place of layer 1, W1/b1 grads.
+//   backward head weights (lane = k), dL/dz2 in place of the layer-2 activations (rows >= B
+//            zeroed), then per wave one 32 x 32 tile of both W2 grads and dL/dh1 (MFMA), dL/dz1
+//            in place of layer 1 after a barrier, W1 grads (one 16 x 16 MFMA tile per wave).
 //   update   global grad 2-norm (block reduction), clip, Adam with bias correction.
 #pragma clang fp contract(off)
 
@@ -39,17 +43,27 @@ constexpr int kNW = kPT / 64;                   // waves
 constexpr int kRow = kHid + 1;                  // padded activation row
 constexpr int kMaxP = 9680;                     // >= policy_param_count(8) = 9,669
 constexpr int kPerT = (kMaxP + kPT - 1) / kPT;  // parameters owned per thread (Adam moments)
+constexpr int kMaxPL = kMaxP + kMaxP / 64 + 1;  // padded LDS image of kMaxP parameters
+
+// Parameter p lives at LDS float lx(p): one pad float after every 64.  Every 64 x 64 hidden
+// weight block starts at a multiple of 64 (PLayout: the blocks before it are 64 (D + 1) floats),
+// so its rows land at stride 65 = kRow and MFMA operand reads down a column or along a row hit
+// 64 distinct banks.
+__device__ __forceinline__ int lx(int p) { return p + (p >> 6); }
 
 // LDS layout (floats)
-constexpr int oPW = 0;                        // [kMaxP] parameters
-constexpr int oPG = oPW + kMaxP;              // [kMaxP] gradients
-constexpr int oPO = oPG + kMaxP;              // [kPB][9] observations (zero-padded to 8)
+constexpr int oPW = 0;                        // [kMaxPL] parameters (padded image, lx)
+constexpr int oPG = oPW + kMaxPL;             // [kMaxPL] gradients (same image)
+constexpr int oPO = oPG + kMaxPL;             // [kPB][9] observations (zero-padded to 8)
 constexpr int oPH1 = oPO + kPB * 9;           // [2][kPB][kRow] layer-1 tanh, then dL/dz1
 constexpr int oPH2 = oPH1 + 2 * kPB * kRow;   // [2][kPB][kRow] layer-2 tanh, then dL/dz2
 constexpr int oPS = oPH2 + 2 * kPB * kRow;    // [16][kPB] per-sample scalars
 constexpr int oPR = oPS + 16 * kPB;           // [64] reduction scratch
 constexpr int kPPOLds = oPR + 64;
 constexpr size_t kPPOLdsBytes = (size_t)kPPOLds * sizeof(float);
+static_assert(kPPOLdsBytes <= 160 * 1024, "fused PPO update exceeds the 160 KiB LDS of a CU");
+static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
+              "parameter image too small for D = 8");
 
 // per-sample scalar slots
 enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV };
@@ -70,6 +84,9 @@ __device__ __forceinline__ float wsum(float v) {
     return v;
 }
 
+#ifndef FENV_PPO_DUMP_GRAD
+#define FENV_PPO_DUMP_GRAD 0
+#endif
 #ifndef FENV_PPO_PROFILE
 #define FENV_PPO_PROFILE 0  // 1: per-phase shader-clock totals -> stats[4..15] (diagnostic build)
 #endif
@@ -95,7 +112,11 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
     const int P = L.total;
     const ppo_hparams hp = g.hp;
 
-    for (int p = tid; p < P; p += kPT) W[p] = g.params[p];
+    for (int p = tid; p < P; p += kPT) W[lx(p)] = g.params[p];
+    // activations and observations start finite: the MFMA contractions run over all 64 rows
+    // and a partial minibatch's unused rows (multiplied by zeros) must not hold NaN bit patterns
+    for (int q = tid; q < 4 * kPB * kRow; q += kPT) H1[q] = 0.0f;  // H1 and H2 are contiguous
+    for (int q = tid; q < kPB * 9; q += kPT) O[q] = 0.0f;
     float m[kPerT], v[kPerT];  // Adam moments of the parameters this thread owns
 #pragma unroll
     for (int q = 0; q < kPerT; ++q) {
@@ -146,46 +167,42 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             if (lane < B) {
                 for (int u = w; u < 2 * kHid; u += kNW) {
                     const int net = u >> 6, j = u & 63;
-                    const float *w1 = W + (net ? L.vf0W : L.pi0W) + j * D;
-                    float z = W[(net ? L.vf0b : L.pi0b) + j];
-                    // 8 terms always: obs is zero-padded past D, so the extra w1[i] * 0 add nothing
+                    const int w1 = (net ? L.vf0W : L.pi0W) + j * D;
+                    float z = W[lx((net ? L.vf0b : L.pi0b) + j)];
+                    // 8 terms always: obs is zero-padded past D, so the extra w1[i] * 0 add
+                    // nothing (w1 + i past the row stays inside the parameter image)
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) z = __builtin_fmaf(w1[i], O[lane * 9 + i], z);
+                    for (int i = 0; i < 8; ++i) z = __builtin_fmaf(W[lx(w1 + i)], O[lane * 9 + i], z);
                     H1[(net * kPB + lane) * kRow + j] = tanhf(z);
                 }
             }
             __syncthreads();
             FENV_PPO_PHASE(1);
-            // ---- layer 2: lane = sample, 8 units per wave; per 4 k one h read per k and one
-            // broadcast ds_read_b128 of W2 per unit (the fmaf chain over k keeps its order)
-            for (int grp = w; grp < 16 && lane < B; grp += kNW) {
-                const int net = (8 * grp) >> 6, j0 = (8 * grp) & 63;
-                const float *w2 = W + (net ? L.vf2W : L.pi2W) + j0 * kHid;
-                const float *h = H1 + (net * kPB + lane) * kRow;
-                float acc[8];
+            // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
+            // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
+            // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
+            {
+                const int net = w >> 2, mt = (w >> 1) & 1, nt = w & 1, h = lane >> 5;
+                const int c = lane & 31;
+                const float *Ar = H1 + (net * kPB + 32 * mt + c) * kRow + 32 * h;
+                const float *Bc = W + lx(net ? L.vf2W : L.pi2W) + (32 * nt + c) * kRow + 32 * h;
+                const float bias = W[lx((net ? L.vf2b : L.pi2b) + 32 * nt + c)];
+                f32x16 acc;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) acc[u] = W[(net ? L.vf2b : L.pi2b) + j0 + u];
-#pragma unroll 4
-                for (int k = 0; k < kHid; k += 4) {
-                    const float h0 = h[k], h1 = h[k + 1], h2 = h[k + 2], h3 = h[k + 3];
+                for (int r = 0; r < 16; ++r) acc[r] = bias;
+#pragma unroll 8
+                for (int i = 0; i < 32; ++i)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ar[i], Bc[i], acc, 0, 0, 0);
+                float *Hr = H2 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const f32x4 wv = *reinterpret_cast<const f32x4 *>(w2 + u * kHid + k);
-                        acc[u] = __builtin_fmaf(wv[0], h0, acc[u]);
-                        acc[u] = __builtin_fmaf(wv[1], h1, acc[u]);
-                        acc[u] = __builtin_fmaf(wv[2], h2, acc[u]);
-                        acc[u] = __builtin_fmaf(wv[3], h3, acc[u]);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) H2[(net * kPB + lane) * kRow + j0 + u] = tanhf(acc[u]);
+                for (int r = 0; r < 16; ++r) Hr[rho(r, h) * kRow] = tanhf(acc[r]);
             }
             __syncthreads();
             FENV_PPO_PHASE(2);
             // ---- heads, losses and per-sample gradients (wave 0, lane = sample)
             if (w == 0) {
                 const bool on = lane < B;
-                const float ls0 = W[L.logstd], ls1 = W[L.logstd + 1];
+                const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
                 const float sd0 = expf(ls0), sd1 = expf(ls1);
                 const float var0 = sd0 * sd0, var1 = sd1 * sd1;
                 const float lsd0 = logf(sd0), lsd1 = logf(sd1);  // torch: std.log()
@@ -195,13 +212,13 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     const float *ha = H2 + lane * kRow, *hv = H2 + (kPB + lane) * kRow;
                     float mu0 = 0.f, mu1 = 0.f, val = 0.f;
                     for (int k = 0; k < kHid; ++k) {
-                        mu0 = __builtin_fmaf(W[L.actW + k], ha[k], mu0);
-                        mu1 = __builtin_fmaf(W[L.actW + kHid + k], ha[k], mu1);
-                        val = __builtin_fmaf(W[L.valW + k], hv[k], val);
+                        mu0 = __builtin_fmaf(W[lx(L.actW + k)], ha[k], mu0);
+                        mu1 = __builtin_fmaf(W[lx(L.actW + kHid + k)], ha[k], mu1);
+                        val = __builtin_fmaf(W[lx(L.valW + k)], hv[k], val);
                     }
-                    mu0 += W[L.actb];
-                    mu1 += W[L.actb + 1];
-                    val += W[L.valb];
+                    mu0 += W[lx(L.actb)];
+                    mu1 += W[lx(L.actb + 1)];
+                    val += W[lx(L.valb)];
                     const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
                     const float d0 = a0 - mu0, d1 = a1 - mu1;
                     const float kLogSqrt2Pi = 0.918938533204672742f;
@@ -245,11 +262,11 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     st_el += (double)(-ent);
                     st_cf += (double)(cf * invB);
                     // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls = 1)
-                    G[L.logstd] = gls0 - hp.ent_coef;
-                    G[L.logstd + 1] = gls1 - hp.ent_coef;
-                    G[L.actb] = sgmu0;
-                    G[L.actb + 1] = sgmu1;
-                    G[L.valb] = sgv;
+                    G[lx(L.logstd)] = gls0 - hp.ent_coef;
+                    G[lx(L.logstd + 1)] = gls1 - hp.ent_coef;
+                    G[lx(L.actb)] = sgmu0;
+                    G[lx(L.actb + 1)] = sgmu1;
+                    G[lx(L.valb)] = sgv;
                 }
             }
             __syncthreads();
@@ -261,84 +278,89 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 float acc = 0.f;
 #pragma unroll 8
                 for (int b = 0; b < B; ++b) acc = __builtin_fmaf(S[slot * kPB + b], h[b * kRow + lane], acc);
-                G[(w == 2 ? L.valW : L.actW + w * kHid) + lane] = acc;
+                G[lx((w == 2 ? L.valW : L.actW + w * kHid) + lane)] = acc;
             }
             __syncthreads();
             FENV_PPO_PHASE(4);
-            // ---- dL/dz2 in place (pairs (net, b): wave w handles 8 of them, lane = k)
+            // ---- dL/dz2 in place (pairs (net, b): wave w handles 16 of them, lane = k); rows
+            // b >= B are zeroed so the contractions over all 64 samples ignore them
             for (int pr = w; pr < 2 * kPB; pr += kNW) {
                 const int net = pr >> 6, b = pr & 63;
+                float *hp2 = H2 + (net * kPB + b) * kRow + lane;
                 if (b < B) {
-                    float *hp2 = H2 + (net * kPB + b) * kRow + lane;
-                    const float gh = net ? S[sGV * kPB + b] * W[L.valW + lane]
-                                         : S[sGMU0 * kPB + b] * W[L.actW + lane] +
-                                               S[sGMU1 * kPB + b] * W[L.actW + kHid + lane];
+                    const float gh = net ? S[sGV * kPB + b] * W[lx(L.valW + lane)]
+                                         : S[sGMU0 * kPB + b] * W[lx(L.actW + lane)] +
+                                               S[sGMU1 * kPB + b] * W[lx(L.actW + kHid + lane)];
                     const float h = *hp2;
                     *hp2 = gh * (1.0f - h * h);
+                } else {
+                    *hp2 = 0.0f;
                 }
             }
             __syncthreads();
             FENV_PPO_PHASE(5);
-            // ---- W2 gradients (rows (net, j0..j0+7) per wave, lane = k): one h1 read and 8
-            // broadcast dL/dz2 reads per sample
-            for (int grp = w; grp < 16; grp += kNW) {
-                const int net = (8 * grp) >> 6, j0 = (8 * grp) & 63;
-                float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-                for (int b = 0; b < B; ++b) {
-                    const float hk = H1[(net * kPB + b) * kRow + lane];
-                    const float *z2 = H2 + (net * kPB + b) * kRow + j0;
+            // ---- W2 gradients GW2 = dZ2^T . H1 and dL/dh1 = dZ2 . W2, both on
+            // v_mfma_f32_32x32x2f32 with K = 64 (samples b resp. hidden j; slot h <-> 32h + i).
+            // Wave w owns tile (net w>>2, rows 32((w>>1)&1), cols 32(w&1)) of each; dL/dz1
+            // overwrites H1 only after the barrier (GW2 reads H1).
+            {
+                const int net = w >> 2, mt = (w >> 1) & 1, nt = w & 1, h = lane >> 5;
+                const int c = lane & 31;
+                const int w2 = lx(net ? L.vf2W : L.pi2W);
+                const float *Z2 = H2 + net * kPB * kRow;  // dL/dz2 [b][j]
+                const float *A1 = H1 + net * kPB * kRow;  // h1 [b][k]
+                f32x16 gw, dz;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) acc[u] = __builtin_fmaf(z2[u], hk, acc[u]);
+                for (int r = 0; r < 16; ++r) gw[r] = dz[r] = 0.0f;
+#pragma unroll 4
+                for (int i = 0; i < 32; ++i) {
+                    const int kk = 32 * h + i;
+                    gw = __builtin_amdgcn_mfma_f32_32x32x2f32(Z2[kk * kRow + 32 * mt + c],
+                                                             A1[kk * kRow + 32 * nt + c], gw, 0, 0, 0);
+                    dz = __builtin_amdgcn_mfma_f32_32x32x2f32(Z2[(32 * mt + c) * kRow + kk],
+                                                             W[w2 + kk * kRow + 32 * nt + c], dz,
+                                                             0, 0, 0);
                 }
+                float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    G[(net ? L.vf2W : L.pi2W) + (j0 + u) * kHid + lane] = acc[u];
-            }
-            if (tid < 2 * kHid) {
-                const int net = tid >> 6, j = tid & 63;
-                const float *z2 = H2 + net * kPB * kRow + j;
-                float acc = 0.f;
+                for (int r = 0; r < 16; ++r) Gr[rho(r, h) * kRow] = gw[r];
+                if (tid < 2 * kHid) {
+                    const int bn = tid >> 6, j = tid & 63;
+                    const float *z2 = H2 + bn * kPB * kRow + j;
+                    float acc = 0.f;
 #pragma unroll 8
-                for (int b = 0; b < B; ++b) acc += z2[b * kRow];
-                G[(net ? L.vf2b : L.pi2b) + j] = acc;
-            }
-            __syncthreads();
-            FENV_PPO_PHASE(6);
-            // ---- dL/dz1 in place of layer 1 (8 (net, b) pairs per wave, lane = k): one W2 read
-            // and 8 broadcast dL/dz2 reads per hidden row j
-            for (int grp = w; grp < 16; grp += kNW) {
-                const int net = (8 * grp) >> 6, b0 = (8 * grp) & 63;
-                if (b0 >= B) continue;
-                const float *w2 = W + (net ? L.vf2W : L.pi2W) + lane;
-                const float *z2 = H2 + (net * kPB + b0) * kRow;
-                float gh[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-                for (int j = 0; j < kHid; ++j) {
-                    const float wk = w2[j * kHid];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) gh[q] = __builtin_fmaf(wk, z2[q * kRow + j], gh[q]);
+                    for (int b = 0; b < B; ++b) acc += z2[b * kRow];
+                    G[lx((bn ? L.vf2b : L.pi2b) + j)] = acc;
                 }
+                __syncthreads();
+                FENV_PPO_PHASE(6);
+                float *H1r = H1 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    if (b0 + q < B) {
-                        float *hp1 = H1 + (net * kPB + b0 + q) * kRow + lane;
-                        const float h = *hp1;
-                        *hp1 = gh[q] * (1.0f - h * h);
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const float hv = H1r[rho(r, h) * kRow];
+                    H1r[rho(r, h) * kRow] = dz[r] * (1.0f - hv * hv);
                 }
             }
             __syncthreads();
             FENV_PPO_PHASE(7);
-            // ---- W1 gradients (one (net, j, i) per thread) and b1 gradients
-            for (int t = tid; t < 2 * kHid * 8; t += kPT) {
-                const int net = t >> 9, j = (t >> 3) & 63, i = t & 7;
-                if (i < D) {
-                    const float *z1 = H1 + net * kPB * kRow + j;
-                    float acc = 0.f;
-#pragma unroll 8
-                    for (int b = 0; b < B; ++b) acc = __builtin_fmaf(z1[b * kRow], O[b * 9 + i], acc);
-                    G[(net ? L.vf0W : L.pi0W) + j * D + i] = acc;
+            // ---- W1 gradients GW1 = dZ1^T . O on v_mfma_f32_16x16x4f32 (wave w: net w>>2, hidden
+            // rows 16(w&3)..+15, obs columns 0..15 of which 0..D-1 are real; K = 64 samples,
+            // slot q <-> sample 16q + i) and b1 gradients
+            {
+                const int net = w >> 2, jt = w & 3, q = lane >> 4, c = lane & 15;
+                const float *Z1 = H1 + net * kPB * kRow + 16 * jt + c;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int b = 16 * q + i;
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Z1[b * kRow],
+                                                              c < 8 ? O[b * 9 + c] : 0.0f, acc,
+                                                              0, 0, 0);
+                }
+                if (c < D) {
+                    const int w1 = (net ? L.vf0W : L.pi0W) + (16 * jt + 4 * q) * D + c;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) G[lx(w1 + r * D)] = acc[r];
                 }
             }
             if (tid < 2 * kHid) {
@@ -347,7 +369,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 float acc = 0.f;
 #pragma unroll 8
                 for (int b = 0; b < B; ++b) acc += z1[b * kRow];
-                G[(net ? L.vf0b : L.pi0b) + j] = acc;
+                G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
             }
             __syncthreads();
             FENV_PPO_PHASE(8);
@@ -356,7 +378,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
             for (int q = 0; q < kPerT; ++q) {
                 const int p = tid + q * kPT;
-                if (p < P) ss = __builtin_fmaf(G[p], G[p], ss);
+                if (p < P) ss = __builtin_fmaf(G[lx(p)], G[lx(p)], ss);
             }
             ss = wsum(ss);
             if (lane == 0) R[w] = ss;
@@ -377,24 +399,31 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             for (int q = 0; q < kPerT; ++q) {
                 const int p = tid + q * kPT;
                 if (p < P) {
-                    const float gr = G[p] * coef;
+                    const float gr = G[lx(p)] * coef;
                     m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
                     v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
                     const float den = __builtin_sqrtf(v[q]) / bc2s + hp.eps;
-                    W[p] = W[p] - step_size * (m[q] / den);
+                    W[lx(p)] = W[lx(p)] - step_size * (m[q] / den);
                 }
             }
             __syncthreads();
             FENV_PPO_PHASE(10);
         }
     }
-    for (int p = tid; p < P; p += kPT) g.params[p] = W[p];
+    for (int p = tid; p < P; p += kPT) g.params[p] = W[lx(p)];
 #pragma unroll
     for (int q = 0; q < kPerT; ++q) {
         const int p = tid + q * kPT;
         if (p < P) {
+#if FENV_PPO_DUMP_GRAD  // diagnostic build: the last minibatch's unclipped gradient, its
+                        // observations and dL/dz1 rows
+            g.exp_avg[p] = G[lx(p)];
+            g.exp_avg_sq[p] = p < kPB * 9 ? O[p] : (p < kPB * 9 + 2 * kPB * kHid
+                ? H1[((p - kPB * 9) >> 6) * kRow + ((p - kPB * 9) & 63)] : 0.0f);
+#else
             g.exp_avg[p] = m[q];
             g.exp_avg_sq[p] = v[q];
+#endif
         }
     }
     if (tid == 0) {
