@@ -17,15 +17,16 @@
 // operand reads are bank-conflict free.  Results match the torch path to summation-order
 // rounding (tests/test_gpu_rollout.py).
 //
-// Work split per minibatch (B <= 64 samples, 8 waves, 2 per SIMD):
-//   forward  layer 1: lane = sample, 16 hidden units per wave (VALU, 8-deep);
-//            layer 2: wave w = one 32 x 32 tile (net, sample rows, hidden cols), 32 MFMAs.
-//            Activation rows are padded to 65 floats; all 64 rows run (rows >= B are unused).
-//   loss     wave 0, lane = sample: heads, log-prob, ratio, clipped surrogate, value loss, and the
+// Work split per minibatch (B <= 64 samples, 8 waves, 2 per SIMD); every contraction runs over
+// all 64 sample rows (rows >= B hold finite stale values and are multiplied by zeroed dL/dz):
+//   forward  layer 1: one 16-unit x 64-sample block per wave (16x16x4 MFMA, K = 8);
+//            layer 2: one 32 x 32 tile (net, sample rows, hidden cols) per wave, 32 MFMAs;
+//            heads mu / value: one 16-sample tile per wave (16x16x4, K = 64) -> per-sample slots.
+//   loss     wave 0, lane = sample: log-prob, ratio, clipped surrogate, value loss, and the
 //            per-sample gradients w.r.t. mu, value, log_std (torch's min/clamp subgradients).
-//   backward head weights (lane = k), dL/dz2 in place of the layer-2 activations (rows >= B
-//            zeroed), then per wave one 32 x 32 tile of both W2 grads and dL/dh1 (MFMA), dL/dz1
-//            in place of layer 1 after a barrier, W1 grads (one 16 x 16 MFMA tile per wave).
+//   backward head weight grads (16x16x4 tile of hidden rows per wave) and dL/dz2 in place of the
+//            same wave's H2 columns (rows >= B zeroed); one 32 x 32 tile of both W2 grads and
+//            dL/dh1 per wave, dL/dz1 in place of layer 1 after a barrier; W1 grads (16x16x4).
 //   update   global grad 2-norm (block reduction), clip, Adam with bias correction.
 #pragma clang fp contract(off)
 
@@ -66,7 +67,7 @@ static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
               "parameter image too small for D = 8");
 
 // per-sample scalar slots
-enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV };
+enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV, sMU0, sMU1, sVAL };
 
 struct PPOArgs {
     float *params, *exp_avg, *exp_avg_sq, *step;
@@ -164,16 +165,24 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const float sd = __builtin_sqrtf(wsum(d * d) / (float)(B - 1));
                 if (lane < B) S[sADV * kPB + lane] = (a - mean) / (sd + 1e-8f);
             }
-            if (lane < B) {
-                for (int u = w; u < 2 * kHid; u += kNW) {
-                    const int net = u >> 6, j = u & 63;
-                    const int w1 = (net ? L.vf0W : L.pi0W) + j * D;
-                    float z = W[lx((net ? L.vf0b : L.pi0b) + j)];
-                    // 8 terms always: obs is zero-padded past D, so the extra w1[i] * 0 add
-                    // nothing (w1 + i past the row stays inside the parameter image)
+            // layer 1 on v_mfma_f32_16x16x4f32: wave w = net w>>2, hidden units 16(w&3)..+15, all
+            // 64 sample rows as 4 tiles; K = 8 obs columns (zero-padded past D) as 2 MFMAs.  The
+            // W1 operand past column D reads the next row's weights, multiplied by O's zeros.
+            {
+                const int net = w >> 2, jt = w & 3, q = lane >> 4, c = lane & 15;
+                const int j = 16 * jt + c;
+                const int w1 = (net ? L.vf0W : L.pi0W) + j * D + q;
+                const float b0 = W[lx(w1)], b1 = W[lx(w1 + 4)];
+                const float bias = W[lx((net ? L.vf0b : L.pi0b) + j)];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) z = __builtin_fmaf(W[lx(w1 + i)], O[lane * 9 + i], z);
-                    H1[(net * kPB + lane) * kRow + j] = tanhf(z);
+                for (int bt = 0; bt < 4; ++bt) {
+                    const float *o = O + (16 * bt + c) * 9 + q;
+                    f32x4 acc = {bias, bias, bias, bias};
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[0], b0, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[4], b1, acc, 0, 0, 0);
+                    float *hr = H1 + (net * kPB + 16 * bt + 4 * q) * kRow + j;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hr[r * kRow] = tanhf(acc[r]);
                 }
             }
             __syncthreads();
@@ -198,6 +207,28 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 for (int r = 0; r < 16; ++r) Hr[rho(r, h) * kRow] = tanhf(acc[r]);
             }
             __syncthreads();
+            // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
+            // v_mfma_f32_16x16x4f32: wave w = net w>>2, samples 16(w&3)..+15, output columns 0..15
+            // of which 2 (actor) / 1 (critic) are real; K = 64 hidden as 16 MFMAs
+            {
+                const int net = w >> 2, bt = w & 3, q = lane >> 4, c = lane & 15;
+                const int ncol = net ? 1 : 2;
+                const float *a = H2 + (net * kPB + 16 * bt + c) * kRow + q;
+                const int hw = net ? L.valW : L.actW + (c & 1) * kHid;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s4 = 0; s4 < 16; ++s4) {
+                    const float bw = c < ncol ? W[lx(hw + 4 * s4 + q)] : 0.0f;
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4], bw, acc, 0, 0, 0);
+                }
+                if (c < ncol) {
+                    const float hb = W[lx(net ? L.valb : L.actb + c)];
+                    float *so = S + (net ? sVAL : sMU0 + c) * kPB + 16 * bt + 4 * q;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) so[r] = acc[r] + hb;
+                }
+            }
+            __syncthreads();
             FENV_PPO_PHASE(2);
             // ---- heads, losses and per-sample gradients (wave 0, lane = sample)
             if (w == 0) {
@@ -209,16 +240,8 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
                 if (on) {
-                    const float *ha = H2 + lane * kRow, *hv = H2 + (kPB + lane) * kRow;
-                    float mu0 = 0.f, mu1 = 0.f, val = 0.f;
-                    for (int k = 0; k < kHid; ++k) {
-                        mu0 = __builtin_fmaf(W[lx(L.actW + k)], ha[k], mu0);
-                        mu1 = __builtin_fmaf(W[lx(L.actW + kHid + k)], ha[k], mu1);
-                        val = __builtin_fmaf(W[lx(L.valW + k)], hv[k], val);
-                    }
-                    mu0 += W[lx(L.actb)];
-                    mu1 += W[lx(L.actb + 1)];
-                    val += W[lx(L.valb)];
+                    const float mu0 = S[sMU0 * kPB + lane], mu1 = S[sMU1 * kPB + lane];
+                    const float val = S[sVAL * kPB + lane];
                     const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
                     const float d0 = a0 - mu0, d1 = a1 - mu1;
                     const float kLogSqrt2Pi = 0.918938533204672742f;
@@ -271,33 +294,47 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(3);
-            // ---- head weight gradients (waves 0-2, lane = hidden unit k)
-            if (w < 3) {
-                const int slot = w == 0 ? sGMU0 : (w == 1 ? sGMU1 : sGV);
-                const float *h = H2 + (w == 2 ? kPB : 0) * kRow;
-                float acc = 0.f;
-#pragma unroll 8
-                for (int b = 0; b < B; ++b) acc = __builtin_fmaf(S[slot * kPB + b], h[b * kRow + lane], acc);
-                G[lx((w == 2 ? L.valW : L.actW + w * kHid) + lane)] = acc;
-            }
-            __syncthreads();
-            FENV_PPO_PHASE(4);
-            // ---- dL/dz2 in place (pairs (net, b): wave w handles 16 of them, lane = k); rows
-            // b >= B are zeroed so the contractions over all 64 samples ignore them
-            for (int pr = w; pr < 2 * kPB; pr += kNW) {
-                const int net = pr >> 6, b = pr & 63;
-                float *hp2 = H2 + (net * kPB + b) * kRow + lane;
-                if (b < B) {
-                    const float gh = net ? S[sGV * kPB + b] * W[lx(L.valW + lane)]
-                                         : S[sGMU0 * kPB + b] * W[lx(L.actW + lane)] +
-                                               S[sGMU1 * kPB + b] * W[lx(L.actW + kHid + lane)];
-                    const float h = *hp2;
-                    *hp2 = gh * (1.0f - h * h);
-                } else {
-                    *hp2 = 0.0f;
+            // ---- head weight gradients on v_mfma_f32_16x16x4f32 (wave w = net w>>2, hidden rows
+            // 16(w&3)..+15, columns gmu0/gmu1 resp. gv; K = 64 samples as 16 MFMAs), then
+            // dL/dz2 in place over the SAME H2 columns (only this wave reads or writes them in
+            // this phase, so no barrier between); rows b >= B are zeroed so the contractions
+            // over all 64 samples ignore them
+            {
+                const int net = w >> 2, kt = w & 3, q = lane >> 4, c = lane & 15;
+                const int ncol = net ? 1 : 2;
+                float *hcol = H2 + net * kPB * kRow + 16 * kt;
+                const float *sg = S + (net ? sGV : sGMU0 + (c & 1)) * kPB;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s4 = 0; s4 < 16; ++s4) {
+                    const int b = 4 * s4 + q;
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hcol[b * kRow + c],
+                                                              c < ncol ? sg[b] : 0.0f, acc, 0, 0, 0);
+                }
+                if (c < ncol) {
+                    const int hw = net ? L.valW : L.actW + c * kHid;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) G[lx(hw + 16 * kt + 4 * q + r)] = acc[r];
+                }
+                const int k = 16 * kt + c;
+                const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
+                const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
+#pragma unroll 4
+                for (int t = 0; t < 16; ++t) {
+                    const int b = 4 * t + q;
+                    float *hp2 = hcol + b * kRow + c;
+                    float v = 0.0f;
+                    if (b < B) {
+                        const float gh = net ? S[sGV * kPB + b] * wa0
+                                             : S[sGMU0 * kPB + b] * wa0 + S[sGMU1 * kPB + b] * wa1;
+                        const float hv = *hp2;
+                        v = gh * (1.0f - hv * hv);
+                    }
+                    *hp2 = v;
                 }
             }
             __syncthreads();
+            FENV_PPO_PHASE(4);
             FENV_PPO_PHASE(5);
             // ---- W2 gradients GW2 = dZ2^T . H1 and dL/dh1 = dZ2 . W2, both on
             // v_mfma_f32_32x32x2f32 with K = 64 (samples b resp. hidden j; slot h <-> 32h + i).
@@ -394,7 +431,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
             const float bc2 = 1.0f - exp2f(step * lb2);
             const float step_size = hp.lr / bc1;
-            const float bc2s = __builtin_sqrtf(bc2);
+            const float inv_bc2s = 1.0f / __builtin_sqrtf(bc2);
 #pragma unroll
             for (int q = 0; q < kPerT; ++q) {
                 const int p = tid + q * kPT;
@@ -402,8 +439,10 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     const float gr = G[lx(p)] * coef;
                     m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
                     v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
-                    const float den = __builtin_sqrtf(v[q]) / bc2s + hp.eps;
-                    W[lx(p)] = W[lx(p)] - step_size * (m[q] / den);
+                    // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
+                    // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
+                    const float den = __builtin_amdgcn_sqrtf(v[q]) * inv_bc2s + hp.eps;
+                    W[lx(p)] = W[lx(p)] - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
                 }
             }
             __syncthreads();

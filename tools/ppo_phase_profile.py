@@ -30,7 +30,7 @@ m.train()
 torch.cuda.synchronize()
 n = env.num_envs * 10
 mb = 10 * -(-n // 64)
-names = ["gather", "advnorm+layer1", "layer2", "loss", "head grads", "dz2", "W2 grads", "dz1",
+names = ["gather", "advnorm+layer1", "layer2+heads", "loss", "head grads+dz2", "-", "W2 grads+dh1", "dz1 store",
          "W1 grads", "norm reduce", "adam"]
 tot = 0.0
 for k, v in zip(names, m._sums[4:15].tolist()):
