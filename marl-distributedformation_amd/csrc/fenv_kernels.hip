@@ -42,6 +42,18 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
 #ifndef FENV_RS_OCC
 #define FENV_RS_OCC
 #endif
+// XCD-aware slice order (FENV_RS_XCD=1): workgroups are dispatched round-robin over the 8 XCDs
+// (block b -> XCD b % 8), so by default neighbouring slices -- whose 480-B done rows share
+// 128-B lines -- sit in different XCDs' L2s.  The remap gives each XCD one contiguous range of
+// slices (blocks b, b + 8, b + 16, ... -> consecutive slices).
+#ifndef FENV_RS_XCD
+#define FENV_RS_XCD 0
+#endif
+__device__ __forceinline__ int64_t xcd_slice(int64_t b, int64_t nb) {
+    if (!FENV_RS_XCD) return b;
+    const int64_t x = b & 7, q = nb >> 3, r = nb & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
 constexpr int kRS = 8;
 constexpr int kRSA = 64 * kRS;
 constexpr int kRSTB = FENV_RS_TB;
@@ -113,7 +125,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
 #ifndef FENV_ACT_PREFETCH
 #define FENV_ACT_PREFETCH 1
 #endif
-    constexpr int kPF = RA ? 1 : FENV_ACT_PREFETCH;
+    constexpr int kPF = (RA || RS) ? 1 : FENV_ACT_PREFETCH;  // staged rows: one-step prefetch
     float2 ring[kPF];
     const int64_t ga = c.f0 * c.N + a;  // global agent index (shard-invariant actions)
     uint4 words = make_uint4(0u, 0u, 0u, 0u);
@@ -157,7 +169,6 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         }
     };
     if (RS) {  // chunks of kRSTB steps, each followed by one workgroup flush of its rows
-        static_assert(!RS || kPF == 1, "staged rows use the one-step prefetch");
 #pragma unroll 1
         for (int32_t kc = 0; kc < T; kc += kRSTB) {
             const int32_t ke = T - kc < kRSTB ? T : kc + kRSTB;
@@ -251,7 +262,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     __shared__ __attribute__((aligned(16))) uint8_t dbuf[kRSTB * kRSA];
     __shared__ float2 red[kRS];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t wave = (int64_t)blockIdx.x * kRS + w;
+    const int64_t blk = xcd_slice(blockIdx.x, gridDim.x);
+    const int64_t wave = blk * kRS + w;
     const int N = c.N;
     const int Mw = c.fpw * N;  // agents of a full wave
     const int fi = lane / N;
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     rsg.rbuf = rbuf;
     rsg.dbuf = dbuf;
     rsg.li = w * Mw + lane;
-    rsg.g0 = (int64_t)blockIdx.x * kRS * Mw;
+    rsg.g0 = blk * kRS * Mw;
     rsg.nwg = (int)((A - rsg.g0) < (int64_t)kRS * Mw ? (A - rsg.g0) : (int64_t)kRS * Mw);
     float rsum = 0.f, dsum = 0.f;
     rollout_body<D, MODE, RA, true>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
@@ -281,8 +293,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
         if (threadIdx.x == 0) {
             float2 v = red[0];
             for (int k = 1; k < kRS; ++k) v = make_float2(v.x + red[k].x, v.y + red[k].y);
-            if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
-            partial[blockIdx.x] = v;
+            if (accum) v = make_float2(partial[blk].x + v.x, partial[blk].y + v.y);
+            partial[blk] = v;
         }
     }
 }
@@ -716,9 +728,23 @@ int64_t group_count(const Consts &c) {
     return c.F;
 }
 
+// Workgroup-staged rows (k_rollout_wave_rs) only where they pay (same-box A/B): a
+// wave's reward row must straddle 128-B lines (agents per wave not a multiple of 32; at N = 64
+// the rows are whole lines and the staging costs 1.4 %), and the grid must be large enough to
+// be store-bound: a small launch (BASELINE config 1, 342 waves) is latency-bound and runs 13 %
+// faster as 4-wave workgroups spread over 4x as many CUs, with no flush barriers.
+#ifndef FENV_RS_MIN_WAVES
+#define FENV_RS_MIN_WAVES 2048
+#endif
+static inline bool use_rs(const Consts &c) {
+    if (!FENV_RS || !wave_path(c.N)) return false;
+    const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
+    return (c.fpw * c.N) % 32 != 0 && waves >= FENV_RS_MIN_WAVES;
+}
+
 int64_t rollout_group_count(const Consts &c) {
     if (FENV_RW && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
-    if (FENV_RS && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRS - 1) / kRS;
+    if (use_rs(c)) return ((c.F + c.fpw - 1) / c.fpw + kRS - 1) / kRS;
     return group_count(c);
 }
 
@@ -731,7 +757,7 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
     if (gen) {  // in-kernel actions
-        if (FENV_RS && wave_path(c.N))
+        if (use_rs(c))
             hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, true>),
                                dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p,
                                T, a2, *gen, obs, rew, done, p2, accum);
@@ -749,7 +775,7 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
         hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
                            dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
                            accum);
-    } else if (FENV_RS && wave_path(c.N)) {
+    } else if (use_rs(c)) {
         hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
                            dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p, T,
                            a2, g0, obs, rew, done, p2, accum);

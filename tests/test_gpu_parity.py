@@ -151,6 +151,13 @@ def test_config2_size_vs_oracle(venv, goal):
     run_vs_oracle(venv, 4096, 5, goal, 9, steps=1010, chunks=[10, 333, 1, 700])
 
 
+@pytest.mark.parametrize("F,N", [(24581, 5), (43013, 3), (12301, 10)])
+def test_staged_kernel_sizes_vs_oracle(venv, F, N):
+    """Grids of >= 2048 waves take the workgroup-staged kernel (k_rollout_wave_rs): ragged last
+    wave and workgroup, single-step launches, launches of 1-3 row flushes, in-launch resets."""
+    run_vs_oracle(venv, F, N, True, 31 + N, steps=40, chunks=[10, 1, 19, 3, 7], max_steps=17)
+
+
 @pytest.mark.parametrize("share", [0.0, 0.1, 0.4, 0.5])
 def test_share_reward_ratio_honoured(venv, share):
     run_vs_oracle(venv, 50, 6, True, 3, steps=30, chunks=[4, 9], max_steps=12, share=share)
@@ -320,15 +327,19 @@ def test_visualize_mirror(venv):
     assert tuple(env._fig.dots[0].center) == (float(px[0]), float(py[0]))
 
 
-@pytest.mark.parametrize("N,mode,T,offset", [(5, "philox", 10, 0), (10, "philox", 7, 3),
-                                              (64, "mt19937", 13, 5), (100, "mt19937", 6, 1),
-                                              (7, "mt19937", 25, 2)])
-def test_rollout_random_actions(venv, N, mode, T, offset):
+@pytest.mark.parametrize("N,mode,T,offset,F", [(5, "philox", 10, 0, 40), (10, "philox", 7, 3, 40),
+                                                (64, "mt19937", 13, 5, 40),
+                                                (100, "mt19937", 6, 1, 40),
+                                                (7, "mt19937", 25, 2, 40),
+                                                # >= 2048 waves: the workgroup-staged kernel
+                                                (5, "mt19937", 12, 4, 30001),
+                                                (10, "philox", 10, 1, 13000)])
+def test_rollout_random_actions(venv, N, mode, T, offset, F):
     """fenv_rollout_random: the in-kernel actions are oracle.philox_actions bit for bit (also
     for a shard), and the rollout equals fenv_rollout fed with those actions from the same state
     -- across MT19937 reset events (max_steps 9) that split the launch."""
     from oracle import philox_actions
-    F, seed = 40, 77
+    seed = 77
     envs = [make_env(venv, F, N, True, 3, reset_mode=mode, max_steps=9) for _ in range(2)]
     for e in envs:
         e.reset_tensor()
