@@ -97,3 +97,34 @@ def max_over_ranks(x: float, device=None) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def world_rank() -> tuple[int, int]:
+    """(world_size, rank) of the initialised process group, (1, 0) without one."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def sample_seed(seed: int, rank: int) -> int:
+    """Philox key of a rank's exploration noise.  The policy kernels key the noise by (local
+    row, step), so ranks sharing one seed would draw identical noise for their k-th agents;
+    rank r uses seed + r * 2^32 instead (rank 0 keeps the single-process stream)."""
+    return (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """Replicate ``t`` from rank ``src`` in place (the policy parameters, once at start)."""
+    world, _ = world_rank()
+    if world > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    """In-place mean over ranks of one flat bucket (the 9,669-float policy gradient)."""
+    world, _ = world_rank()
+    if world > 1:
+        dist.all_reduce(t)
+        t.div_(world)
+    return t

@@ -21,6 +21,7 @@ import torch.distributed as dist
 import torch.nn.functional as Fn
 
 from . import checkpoint as ckpt
+from . import distributed as pdist
 from .policy import MlpPolicy
 from .rollout import RolloutBuffer, RolloutCollector
 
@@ -93,14 +94,18 @@ class PPO:
         self.policy = policy or MlpPolicy(env.obs_dim, device=env.device, seed=seed)
         self.buffer = RolloutBuffer(self.cfg.n_steps, env.num_envs, env.obs_dim, env.device,
                                     self.cfg.gamma, self.cfg.gae_lambda)
-        self.collector = RolloutCollector(env, self.policy, self.buffer, seed=seed)
+        self.world, rank = pdist.world_rank()
+        # replicated weights: rank 0's, once (a loaded checkpoint or seed-identical init alike);
+        # per-rank noise streams (pdist.sample_seed)
+        pdist.broadcast_(self.policy.flat)
+        self.collector = RolloutCollector(env, self.policy, self.buffer,
+                                          seed=pdist.sample_seed(seed, rank))
         self.param = torch.nn.Parameter(self.policy.flat)  # shares storage with the kernel's
         self.param.grad = torch.zeros_like(self.param)     # static: graph replays write it
         # capturable: the step count lives on the device, so the update can be graph-captured
         self.opt = torch.optim.Adam([self.param], lr=self.cfg.learning_rate, eps=1e-5,
                                     capturable=True)
         self.gen = torch.Generator(device=env.device).manual_seed(seed)
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.stats: dict = {}
         # minibatch update as HIP graphs (one replay per minibatch instead of ~60 launches)
         self.use_graph = (self.param.device.type == "cuda") if use_graph is None else use_graph
@@ -151,8 +156,7 @@ class PPO:
 
     def _allreduce(self) -> None:
         if self.world > 1:  # one flat 9,669-float bucket per optimizer step (RCCL)
-            dist.all_reduce(self.param.grad)
-            self.param.grad.div_(self.world)
+            pdist.allreduce_mean_(self.param.grad)
 
     def _eager_step(self, idx: torch.Tensor) -> None:
         self._forward_backward(idx)

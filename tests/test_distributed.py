@@ -66,8 +66,15 @@ def _worker(rank, world, port, root, q):
         red.submit(bufs[k % 2])
     out = red.result().clone()
     mx = d.max_over_ranks(float(rank) * 3.0)
+    # PPO's collectives: rank 0's parameters replicated once, gradient bucket averaged
+    params = torch.full((9669,), float(rank + 1))
+    d.broadcast_(params)
+    grad = torch.arange(9669, dtype=torch.float32) * (rank + 1)
+    d.allreduce_mean_(grad)
+    seeds = [None] * world
+    dist.all_gather_object(seeds, d.sample_seed(12345, rank))
     if rank == 0:
-        q.put((parts, out.tolist(), mx))
+        q.put((parts, out.tolist(), mx, float(params.sum()), grad[:4].tolist(), seeds))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -80,7 +87,7 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q)) for r in range(2)]
     for p in procs:
         p.start()
-    parts, out, mx = q.get(timeout=120)
+    parts, out, mx, psum, g4, seeds = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -97,3 +104,6 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     assert np.array_equal(np.concatenate([np.array(p[2], np.float32) for p in parts]), gx)
     assert out == [float(0 + 4) + float(1 + 4), 2.0]
     assert mx == 3.0
+    assert psum == 9669.0                        # rank 0's ones everywhere
+    assert g4 == [0.0, 1.5, 3.0, 4.5]            # mean of k and 2k
+    assert seeds[0] == 12345 and seeds[1] != seeds[0]  # rank 0 keeps the single-GPU stream
