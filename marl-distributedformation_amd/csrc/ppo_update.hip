@@ -136,25 +136,57 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 
     const int64_t n = g.n;
     const int bs = g.batch_size;
+    // Gather pipeline (B * 8 <= kPT: a thread moves at most one observation value and, for
+    // tid < B, one sample's act / old_log_prob / adv / ret).  The minibatch's values were loaded
+    // into registers during the previous minibatch, from perm indices loaded one minibatch
+    // before that, so no gather waits on a dependent global load (the loop's barriers wait on
+    // LDS only).  Minibatch k = (epoch, start) in the loop's order; kMB = minibatches per epoch.
+    const int64_t kMB = (n + bs - 1) / bs;
+    const int64_t nmb = kMB * (int64_t)g.n_epochs;
+    auto perm_rows = [&](int64_t k, int64_t &ro, int64_t &rs) {  // rows this thread gathers
+        ro = rs = -1;
+        if (k >= nmb) return;
+        const int64_t e = k / kMB, s0k = (k - e * kMB) * bs;
+        const int Bk = (int)((n - s0k) < bs ? (n - s0k) : bs);
+        const int64_t *pp = g.perm + e * n + s0k;
+        if (tid < Bk * 8) ro = pp[tid >> 3];
+        if (tid < Bk) rs = pp[tid];
+    };
+    auto load_rows = [&](int64_t ro, int64_t rs, float &po, float (&ps)[5]) {
+        const int i = tid & 7;
+        po = (ro >= 0 && i < D) ? g.obs[ro * D + i] : 0.0f;
+        if (rs >= 0) {
+            ps[0] = g.act[2 * rs];
+            ps[1] = g.act[2 * rs + 1];
+            ps[2] = g.old_log_prob[rs];
+            ps[3] = g.adv[rs];
+            ps[4] = g.ret[rs];
+        }
+    };
+    float po = 0.0f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    int64_t ro_n, rs_n;  // perm rows of the next minibatch
+    {
+        int64_t ro0, rs0;
+        perm_rows(0, ro0, rs0);
+        load_rows(ro0, rs0, po, ps);
+        perm_rows(1, ro_n, rs_n);
+    }
+    int64_t kmb = 0;
     for (int ep = 0; ep < g.n_epochs; ++ep) {
-        const int64_t *perm = g.perm + (int64_t)ep * n;
-        for (int64_t s0 = 0; s0 < n; s0 += bs) {
+        for (int64_t s0 = 0; s0 < n; s0 += bs, ++kmb) {
             const int B = (int)((n - s0) < bs ? (n - s0) : bs);
             const float invB = 1.0f / (float)B;
-            // ---- gather the minibatch
-            for (int q = tid; q < B * 8; q += kPT) {
-                const int b = q >> 3, i = q & 7;
-                const int64_t r = perm[s0 + b];
-                O[b * 9 + i] = i < D ? g.obs[r * D + i] : 0.0f;
+            // ---- gather the minibatch (from the prefetch registers), then start the next one
+            if (tid < B * 8) O[(tid >> 3) * 9 + (tid & 7)] = po;
+            if (tid < B) {
+                S[sA0 * kPB + tid] = ps[0];
+                S[sA1 * kPB + tid] = ps[1];
+                S[sOLP * kPB + tid] = ps[2];
+                S[sADV * kPB + tid] = ps[3];
+                S[sRET * kPB + tid] = ps[4];
             }
-            for (int b = tid; b < B; b += kPT) {
-                const int64_t r = perm[s0 + b];
-                S[sA0 * kPB + b] = g.act[2 * r];
-                S[sA1 * kPB + b] = g.act[2 * r + 1];
-                S[sOLP * kPB + b] = g.old_log_prob[r];
-                S[sADV * kPB + b] = g.adv[r];
-                S[sRET * kPB + b] = g.ret[r];
-            }
+            load_rows(ro_n, rs_n, po, ps);
+            perm_rows(kmb + 2, ro_n, rs_n);
             __syncthreads();
             FENV_PPO_PHASE(0);
             // ---- advantage normalisation (wave 0) || layer 1 (all waves)
