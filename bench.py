@@ -173,8 +173,11 @@ def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: 
     el = time.perf_counter() - t0
     ms = a.elapsed_time(b) / launches
     byts = rollout_bytes_per_launch(A, agents, 8, T)
-    return {"workload": f"{formations} formations x {agents} agents, fused {T}-step rollouts",
+    shape = (f"fused {T}-step rollouts" if T > 1 else
+             "one env step per launch (fenv_step: state read + write every step)")
+    return {"workload": f"{formations} formations x {agents} agents, {shape}",
             "value": A * T * launches / el, "unit": "agent-steps/s", "avg_kernel_ms": ms,
+            "algorithmic_bytes_per_launch": byts,
             "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
@@ -427,6 +430,9 @@ def main():
                                                                args.formations, N)
             out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
                                   "config4": env_config_bench(pkg.__name__, dev, 16384, 64)}
+            # the single-step face at the headline size: SURVEY §8(d)'s B_step per agent-step
+            out["single_step"] = env_config_bench(pkg.__name__, dev, args.formations, N, 500,
+                                                  T=1)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)

@@ -285,16 +285,21 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     float rsum = 0.f, dsum = 0.f;
     rollout_body<D, MODE, RA, true>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
                                     T, act, gen, obs, rew, done, rsum, dsum, rsg);
-    if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
+    if (partial) {  // one {sum reward, sum done} record per 4 waves -- the same records, in the
+                    // same summation order, as k_rollout_wave's 4-wave workgroups
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
         if (lane == 0) red[w] = make_float2(rsum, dsum);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            float2 v = red[0];
-            for (int k = 1; k < kRS; ++k) v = make_float2(v.x + red[k].x, v.y + red[k].y);
-            if (accum) v = make_float2(partial[blk].x + v.x, partial[blk].y + v.y);
-            partial[blk] = v;
+        const int64_t groups = ((c.F + c.fpw - 1) / c.fpw + 3) / 4;
+        const int hq = (int)threadIdx.x;
+        if (hq < kRS / 4 && blk * (kRS / 4) + hq < groups) {
+            const int64_t gi = blk * (kRS / 4) + hq;
+            float2 v = red[4 * hq];
+            for (int k = 1; k < 4; ++k)
+                v = make_float2(v.x + red[4 * hq + k].x, v.y + red[4 * hq + k].y);
+            if (accum) v = make_float2(partial[gi].x + v.x, partial[gi].y + v.y);
+            partial[gi] = v;
         }
     }
 }
@@ -733,19 +738,29 @@ int64_t group_count(const Consts &c) {
 // the rows are whole lines and the staging costs 1.4 %), and the grid must be large enough to
 // be store-bound: a small launch (BASELINE config 1, 342 waves) is latency-bound and runs 13 %
 // faster as 4-wave workgroups spread over 4x as many CUs, with no flush barriers.
+// A single-step launch pays the flush barrier without amortising it (T = 1: 70.6 µs staged vs
+// 64.2 µs plain at config 3; T = 2-6 tie within 3 % either way).  Both kernels write the same
+// per-4-wave stats records, so the choice may change from launch to launch.
 #ifndef FENV_RS_MIN_WAVES
 #define FENV_RS_MIN_WAVES 2048
 #endif
-static inline bool use_rs(const Consts &c) {
-    if (!FENV_RS || !wave_path(c.N)) return false;
+#ifndef FENV_RS_MIN_T
+#define FENV_RS_MIN_T 2
+#endif
+static inline bool use_rs(const Consts &c, int32_t T) {
+    if (!FENV_RS || !wave_path(c.N) || T < FENV_RS_MIN_T) return false;
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
     return (c.fpw * c.N) % 32 != 0 && waves >= FENV_RS_MIN_WAVES;
 }
 
 int64_t rollout_group_count(const Consts &c) {
     if (FENV_RW && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
-    if (use_rs(c)) return ((c.F + c.fpw - 1) / c.fpw + kRS - 1) / kRS;
     return group_count(c);
+}
+
+// grid of k_rollout_wave_rs: kRS waves per workgroup
+static inline int64_t rs_blocks(const Consts &c) {
+    return ((c.F + c.fpw - 1) / c.fpw + kRS - 1) / kRS;
 }
 
 static inline unsigned block_threads(int32_t N) { return (unsigned)((N + 63) / 64 * 64); }
@@ -757,9 +772,9 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
     if (gen) {  // in-kernel actions
-        if (use_rs(c))
+        if (use_rs(c, T))
             hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, true>),
-                               dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p,
+                               dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p,
                                T, a2, *gen, obs, rew, done, p2, accum);
         else if (wave_path(c.N))
             hipLaunchKernelGGL((k_rollout_wave<D, MODE, true>), dim3((unsigned)group_count(c)),
@@ -775,9 +790,9 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
         hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
                            dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
                            accum);
-    } else if (use_rs(c)) {
+    } else if (use_rs(c, T)) {
         hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
-                           dim3((unsigned)rollout_group_count(c)), dim3(kRSA), 0, st, c, s, p, T,
+                           dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
                            a2, g0, obs, rew, done, p2, accum);
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);

@@ -158,6 +158,31 @@ def test_staged_kernel_sizes_vs_oracle(venv, F, N):
     run_vs_oracle(venv, F, N, True, 31 + N, steps=40, chunks=[10, 1, 19, 3, 7], max_steps=17)
 
 
+def test_stats_records_same_for_both_kernels(venv):
+    """T = 1 launches run k_rollout_wave, longer ones the staged kernel: both write one
+    {sum reward, sum done} record per 4 waves, so one partial buffer serves every launch and
+    the records of a T-step launch equal those of the same steps' rewards summed per group."""
+    F, N = 24581, 5
+    env = make_env(venv, F, N, True, 3, reset_mode="philox", max_steps=4)
+    env.reset_tensor()
+    A = F * N
+    part = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
+    assert env.partial_count() == -(-(-(-F // (64 // N))) // 4)  # ceil(waves / 4)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for T in (1, 6, 1, 3):
+        acts = torch.rand((T, A, 2), device=DEV, generator=g) * 2 - 1
+        obs, rew, done = env.rollout(acts, partial=part)
+        red = env.reduce_partials(part).cpu().double()
+        assert abs(red[0].item() - rew.double().sum().item()) <= 1e-5 * abs(rew.double().sum().item())
+        assert red[1].item() == float(done.sum().item())
+        # per-group records: 4 waves x 60 agents = 240 agents per record
+        per = rew.double().sum(0)
+        pad = torch.zeros(part.shape[0] * 240, dtype=torch.float64, device=DEV)
+        pad[:A] = per
+        ref = pad.view(-1, 240).sum(1)
+        assert torch.allclose(part[:, 0].double(), ref, rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("share", [0.0, 0.1, 0.4, 0.5])
 def test_share_reward_ratio_honoured(venv, share):
     run_vs_oracle(venv, 50, 6, True, 3, steps=30, chunks=[4, 9], max_steps=12, share=share)
