@@ -82,7 +82,8 @@ int fenv_step(fenv_t *env, const float *act, float *obs, float *rew, uint8_t *do
 /* T consecutive env.step calls fused in one launch (state kept on chip): act [T][A][2],
  * obs [T][A][D] (obs[k] = observation returned by step k), rew [T][A], done [T][A].
  * Bit-identical to T fenv_step calls.  partial (may be NULL) receives one {sum reward,
- * sum done} float pair per workgroup (fenv_partial_count of them) for fenv_reduce_partials. */
+ * sum done} float pair per group of 4 wavefronts (N <= 64) or per formation (N > 64) --
+ * fenv_partial_count of them, overwritten by every launch -- for fenv_reduce_partials. */
 int fenv_rollout(fenv_t *env, int32_t T, const float *act, float *obs, float *rew,
                  uint8_t *done, float *partial, void *stream);
 
@@ -98,7 +99,7 @@ int fenv_rollout_random(fenv_t *env, int32_t T, uint64_t act_seed, uint64_t step
                         float *act_out, float *obs, float *rew, uint8_t *done, float *partial,
                         void *stream);
 
-/* Number of float2 partial records fenv_rollout writes (one per workgroup). */
+/* Number of float2 partial records fenv_rollout writes (see fenv_rollout; independent of T). */
 int64_t fenv_partial_count(const fenv_t *env);
 
 /* Deterministic fixed-order reduction of `count` partial records into out[2] (double, device):
