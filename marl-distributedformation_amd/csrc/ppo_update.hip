@@ -41,6 +41,7 @@ namespace fenvk {
 constexpr int kPB = 64;                         // max samples per minibatch
 constexpr int kPT = 512;                        // threads (8 waves; 256-VGPR budget)
 constexpr int kNW = kPT / 64;                   // waves
+static_assert(kNW == 8, "the MFMA tile-to-wave maps below assume 8 waves");
 constexpr int kRow = kHid + 1;                  // padded activation row
 constexpr int kMaxP = 9680;                     // >= policy_param_count(8) = 9,669
 constexpr int kPerT = (kMaxP + kPT - 1) / kPT;  // parameters owned per thread (Adam moments)

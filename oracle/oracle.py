@@ -41,16 +41,31 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
+# Edge-case action components of the "extreme" mode (amp < 0): the env does not clip actions
+# (vectorized_env.py:69-70, quirk Q10), so the step must be exact for signed zeros, subnormal
+# moves off a wall, ±inf / huge pushes that clip exactly onto a wall (then stay "out of bounds"
+# while zero actions hold it there, quirk Q5).  NaN is not among them: NaN payload bits are not
+# an arithmetic result the reference pins.
+EXTREME_ACTIONS = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-39, -1e-39, 1e-30, -1e-30, 3e38, -3e38,
+                            np.inf, -np.inf, 40.0, -40.0, 1.0, -1.0], np.float32)
+
+
 def synth_actions(seed: int, step: int, num_agents: int, amp: float = 1.0) -> np.ndarray:
-    """Deterministic U(-amp, amp) fp32 actions [num_agents, 2] for (seed, step)."""
+    """Deterministic U(-amp, amp) fp32 actions [num_agents, 2] for (seed, step).  amp < 0 is the
+    "extreme" mode: U(-1.2, 1.2) with about half the components replaced by EXTREME_ACTIONS."""
     with np.errstate(over="ignore"):
         base = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15)
                 + np.uint64(step) * np.uint64(0xD1B54A32D192ED03))
         idx = np.arange(2 * num_agents, dtype=np.uint64)
         z = _splitmix64(base + idx)
     u = (z >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
-    a = (u * np.float32(2.0) - np.float32(1.0)) * np.float32(amp)
-    return a.astype(np.float32).reshape(num_agents, 2)
+    a = (u * np.float32(2.0) - np.float32(1.0)) * np.float32(abs(amp) if amp >= 0 else 1.2)
+    a = a.astype(np.float32)
+    if amp < 0:
+        pick = (z & np.uint64(31)).astype(np.int64)  # low bits: independent of u's high bits
+        sel = pick < len(EXTREME_ACTIONS)
+        a[sel] = EXTREME_ACTIONS[pick[sel]]
+    return a.reshape(num_agents, 2)
 
 
 def philox_actions(act_seed: int, step: int, first_agent: int, num_agents: int) -> np.ndarray:

@@ -15,7 +15,8 @@ arrays, logged scalars).  Nothing from the reference's source travels with the r
 
 Per case:
   meta            int64 [F, N, goal_in_obs, seed, act_seed, steps, log]
-  amp             float64 action amplitude (actions = oracle.synth_actions(act_seed, step, A, amp))
+  amp             float64 action amplitude (actions = oracle.synth_actions(act_seed, step, A, amp);
+                  amp < 0 selects its edge-case mode)
   d_nb            float32 desired neighbour distance as the reference holds it
   state_ctor      float32 [A*2 + F*2] agents + goal after the ctor (draw set 1)
   obs_reset       float32 [A, D] from env.reset() (draw set 2)
@@ -100,6 +101,9 @@ CASES = [
     ("f2_n33_d6",         2,    33, False, 32,         22,       1010,  1.0, False, False),
     ("f2_n5_seedmax",     2,    5,  True,  2**32 - 1,  23,       50,    1.0, False, True),
     ("default_cfg_f1000", 1000, 5,  True,  0,          24,       3,     1.0, False, True),
+    # amp < 0: oracle.synth_actions' "extreme" mode (signed zeros, subnormal, huge, +-inf)
+    ("f6_n5_d8_extreme",  6,    5,  True,  77,         25,       1010,  -1.0, True, False),
+    ("f4_n3_d6_extreme",  4,    3,  False, 78,         26,       40,    -1.0, False, True),
 ]
 
 SEL = [1, 2, 3, 500, 1001, 1002, 1003, 2003, 2004, 2005]

@@ -82,7 +82,8 @@ def test_golden_replay_step(venv, name):
 
 
 @pytest.mark.parametrize("name", ["f4_n5_d8", "f2_n64_d8", "f3_n100_d8", "f5_n1_d8",
-                                  "f1_n5_d8_walls", "f3_n10_d6"])
+                                  "f1_n5_d8_walls", "f3_n10_d6", "f6_n5_d8_extreme",
+                                  "f4_n3_d6_extreme"])
 @pytest.mark.parametrize("chunk", [7, 1002, 3000])
 def test_golden_replay_rollout(venv, name, chunk):
     c = gu.load_case(name)
@@ -190,6 +191,16 @@ def test_share_reward_ratio_honoured(venv, share):
 
 def test_out_of_bounds_heavy(venv):
     run_vs_oracle(venv, 200, 5, True, 5, steps=120, chunks=[13], amp=40.0, max_steps=50)
+
+
+@pytest.mark.parametrize("F,N", [(24581, 5), (12, 100), (9, 1024), (301, 1)])
+def test_extreme_actions_vs_oracle(venv, F, N):
+    """Unclipped edge-case actions (signed zeros, subnormal, huge, ±inf; oracle.EXTREME_ACTIONS,
+    pinned against the reference by the *_extreme fixtures) through the staged wave kernel, the
+    workgroup-per-formation kernel and N = 1, across resets."""
+    with np.errstate(over="ignore", invalid="ignore"):
+        run_vs_oracle(venv, F, N, True, 41 + N, steps=30, chunks=[10, 1, 19], amp=-1.0,
+                      max_steps=17)
 
 
 def test_sharded_mt_equals_unsharded(venv):
