@@ -176,3 +176,60 @@ def test_full_size_policy_rollout_sampled(pkg, venv):
         adv_ref[j] = gae
     np.testing.assert_allclose(adv.numpy(), adv_ref, rtol=1e-5, atol=1e-4)
     np.testing.assert_allclose(ret.numpy(), adv_ref + v64, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("F,N,goal,T", [
+    # 3e8 agents, D = 8: obs element offsets pass 2^31 and 2^32 inside row 0 (staged kernel, T=2)
+    (60_000_000, 5, True, 2),
+    # 2.2e9 agents: agent indices pass 2^31 (single-step launches take the plain wave kernel)
+    (440_000_000, 5, False, 1)])
+def test_beyond_int32_sizes_sampled_vs_oracle(venv, F, N, goal, T):
+    """Maximum sizes: batches whose agent or obs-element indices overflow 32 bits (HBM holds
+    them: ~40 GB and ~150 GB here).  In-kernel Philox actions (fenv_rollout_random), sampled
+    formations -- incl. the ones straddling every 2^31 / 2^32 index boundary and the grid's last
+    ones -- replayed by the C oracle bit for bit; the stats records sum to the full reward array."""
+    from oracle import philox_actions
+    env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                             "goal_in_obs": goal}, device=DEV, seed=5, reset_mode="philox")
+    A, D = F * N, env.obs_dim
+    assert A * D > 1 << 31
+    env.reset_tensor()
+    px0, py0, gx0, gy0, t0 = env.get_state()
+    rng = np.random.default_rng(F)
+    edges = [(1 << 31) // (N * D), (1 << 32) // (N * D), (1 << 31) // N, (1 << 32) // N]
+    fs = [rng.choice(F, 1500, replace=False), [0, 1, F - 2, F - 1]]
+    fs += [[e - 1, e, e + 1] for e in edges if e + 1 < F]
+    fs = np.unique(np.concatenate(fs)).astype(np.int64)
+    ag = (fs[:, None] * N + np.arange(N)).reshape(-1)
+    agt, fst = torch.from_numpy(ag).to(DEV), torch.from_numpy(fs).to(DEV)
+    ref = COracleEnv(len(fs), N, goal, 0)
+    ref.set_state(*(v[agt].cpu().numpy() for v in (px0, py0)),
+                  *(v[fst].cpu().numpy() for v in (gx0, gy0, t0)))
+    del px0, py0, gx0, gy0, t0
+    part = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
+    seed = 91
+    if T == 1:  # reuse the env's own [A, D] / [A] buffers (memory)
+        obs, rew, done = env.rollout_random(1, seed, 0, obs=env.obs_dev, rew=env.rew_dev,
+                                            done=env.done_dev, partial=part)
+        obs, rew, done = obs.view(1, A, D), rew.view(1, A), done.view(1, A)
+    else:
+        obs, rew, done = env.rollout_random(T, seed, 0, partial=part)
+    sums = env.reduce_partials(part).cpu().numpy()
+    torch.cuda.synchronize()
+    o_s, r_s, d_s = obs[:, agt].cpu().numpy(), rew[:, agt].cpu().numpy(), done[:, agt].cpu().numpy()
+    for j in range(T):
+        a_j = np.concatenate([philox_actions(seed, j, int(f) * N, N) for f in fs])
+        ro, rr, rd, _ = ref.step(a_j)
+        assert np.array_equal(bits(o_s[j]), bits(ro)), f"obs step {j}"
+        assert np.array_equal(bits(r_s[j]), bits(rr)), f"reward step {j}"
+        assert np.array_equal(d_s[j], rd), f"done step {j}"
+    rs = ref.get_state()
+    px1, py1, gx1, gy1, t1 = env.get_state()
+    for name, v, w, idx in (("px", px1, rs[0], agt), ("py", py1, rs[1], agt),
+                            ("gx", gx1, rs[2], fst), ("gy", gy1, rs[3], fst),
+                            ("t", t1, rs[4], fst)):
+        assert np.array_equal(bits(v[idx].cpu().numpy()), bits(w)), name
+    rsum = rew.double().sum().item()
+    assert abs(sums[0] - rsum) <= 1e-5 * max(1.0, abs(rsum)), (sums[0], rsum)
+    assert sums[1] == 0.0 and not bool(done.any())
+    assert bool((t1 == T).all())
