@@ -410,3 +410,31 @@ def test_rollout_random_actions(venv, N, mode, T, offset, F):
     o3, r3, d3 = envs[0].rollout_random(3, seed, offset + T)
     o4, r4, d4 = envs[1].rollout_random(3, seed, offset + T, act_out=torch.empty_like(act[:3]))
     assert torch.equal(o3, o4) and torch.equal(r3, r4) and torch.equal(d3, d4)
+
+
+@pytest.mark.parametrize("mode", ["mt19937", "philox"])
+def test_empty_launches_are_no_ops(venv, mode):
+    """T = 0 rollouts (actions [0, A, 2]) and T = 0 random rollouts return empty outputs and leave
+    the state -- and the MT19937 reset stream position -- untouched; T < 0 and 0 formations are
+    rejected before any launch."""
+    F, N = 37, 5
+    env = make_env(venv, F, N, True, 8, reset_mode=mode, max_steps=3)
+    ref = make_env(venv, F, N, True, 8, reset_mode=mode, max_steps=3)
+    env.reset_tensor()
+    ref.reset_tensor()
+    A = F * N
+    obs, rew, done = env.rollout(torch.zeros((0, A, 2), dtype=torch.float32, device=DEV))
+    assert obs.shape == (0, A, 8) and rew.shape == (0, A) and done.shape == (0, A)
+    obs, rew, done = env.rollout_random(0, 1, 0)
+    assert obs.numel() == 0
+    for s1, s2 in zip(env.get_state(), ref.get_state()):
+        assert torch.equal(s1, s2)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    acts = torch.rand((9, A, 2), device=DEV, generator=g) * 2 - 1  # crosses two resets
+    o1, r1, d1 = env.rollout(acts)
+    o2, r2, d2 = ref.rollout(acts)
+    assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2) and bool(d1.any())
+    with pytest.raises(Exception):
+        env.rollout_random(-1, 1, 0)
+    with pytest.raises(Exception):
+        make_env(venv, 0, N)
