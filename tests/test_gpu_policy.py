@@ -111,3 +111,25 @@ def test_policy_on_env_observations(pol_mod, venv):
     torch.testing.assert_close(r["value"].cpu(), val, atol=ATOL, rtol=RTOL)
     acts, _ = pol.predict(obs.cpu().numpy())
     assert acts.shape == (5120, 2) and np.all(np.abs(acts) <= 1)
+
+
+def test_batch_beyond_int32_offsets_sampled(pol_mod):
+    """Maximum sizes: 3e8 agents (obs element offsets pass 2^31; ~20 GB of HBM).  Rows are
+    independent, so sampled rows -- incl. those around the 2^31-element boundary and the last,
+    partial tile -- are checked against the oracle."""
+    B, D = 300_000_001, 8
+    pol = pol_mod.MlpPolicy(D, device=DEV, seed=3)
+    sd = randomize(pol, 17)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    obs = torch.rand((B, D), device=DEV, generator=g) * 2.4 - 1.2
+    r = pol.forward(obs, deterministic=True)
+    torch.cuda.synchronize()
+    edge = (1 << 31) // D
+    rows = np.unique(np.concatenate([np.random.default_rng(5).choice(B, 4000, replace=False),
+                                     np.arange(edge - 40, edge + 40), np.arange(B - 70, B),
+                                     [0, 1]]))
+    idx = torch.from_numpy(rows).to(DEV)
+    mu, val = po.forward(sd, obs[idx].cpu())
+    torch.testing.assert_close(r["mu"][idx].cpu(), mu, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["value"][idx].cpu(), val, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(r["clipped"][idx].cpu(), mu.clamp(-1, 1), atol=ATOL, rtol=RTOL)
