@@ -73,19 +73,36 @@ def _cpu_oracle_rate(F: int, N: int, D: int, threads: int, budget_s: float):
     return sum(f * N * k for f, k in zip(shards, steps)) / el, min(steps), el
 
 
+# The reference CPU env itself, measured in the build container:
+# it cannot travel to the GPU box, so it is carried as a labelled constant, never re-run here.
+REFERENCE_CPU_MEASURED = {
+    "value_range": [6.2e3, 1.0e4], "unit": "agent-steps/s",
+    "config": "config0: 1000 formations x 5 agents (cfg/config.yaml defaults)", "threads": 1,
+    "host": "8 vCPU Xeon (KVM), build container", "kind": "reference",
+    "source": "SURVEY.md §6 / BASELINE.md (measured by importing /root/reference; not re-run)"}
+
+
 def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
-    """Time the bit-exact C port of the reference env (oracle/fenv_oracle.c) on a bounded
-    sample of the same workload (random U(-1,1) actions, 5 agents/formation): first 1 thread,
-    then one thread per host core of this job's CPU share (<= 16 on the GPU box) over
-    formation shards.  `value` is the multi-threaded rate; `cores` the threads used."""
+    """Time the bit-exact C port of the reference env (oracle/fenv_oracle.c) on bounded samples:
+    BASELINE config 0 (1000 x 5, the reference's default CPU run) and config 1 (4096 x 5) on one
+    thread, then a sample of the headline workload (65,536 x 5 formations, one thread, then one
+    thread per host core of this job's CPU share, <= 16 on the GPU box, over formation shards).
+    `value` is the multi-threaded rate on the headline sample; `cores` the threads it used."""
     F = 65536
     try:
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count() or 1
     threads = max(1, min(16, share))
-    one, one_steps, one_el = _cpu_oracle_rate(F, N, D, 1, budget_s / 2)
-    many, many_steps, many_el = _cpu_oracle_rate(F, N, D, threads, budget_s / 2)
+    small = budget_s / 6
+    configs = {}
+    for name, (fc, nc) in (("config0", (1000, 5)), ("config1", (4096, 5))):
+        r, k, el = _cpu_oracle_rate(fc, nc, D, 1, small)
+        configs[name] = {"value": r, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+                         "sample": f"{fc} formations x {nc} agents, {k} env steps ({el:.1f} s), "
+                                   f"1 thread"}
+    one, one_steps, one_el = _cpu_oracle_rate(F, N, D, 1, budget_s / 3)
+    many, many_steps, many_el = _cpu_oracle_rate(F, N, D, threads, budget_s / 3)
     return {"value": many, "unit": "agent-steps/s", "cores": threads, "kind": "port",
             "single_thread_value": one,
             "sample": f"{F} formations x {N} agents: 1 thread {one_steps} env steps "
@@ -93,7 +110,9 @@ def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
                       f"shards >= {many_steps} env steps each ({many_el:.1f} s); "
                       f"oracle/fenv_oracle.c (bit-exact C port of simulate.py/"
                       f"vectorized_env.py); host reports {os.cpu_count()} CPUs, "
-                      f"affinity {share}"}
+                      f"affinity {share}",
+            "configs": configs,
+            "reference_measured": REFERENCE_CPU_MEASURED}
 
 
 def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollouts: int) -> dict:
@@ -256,17 +275,37 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
 
 
 def load_pmc_traffic(workload: str):
-    """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json)."""
+    """HBM bytes per launch measured by separate rocprofv3 PMC passes (tools/gpu_pmc.sh ->
+    profiles/pmc_traffic.json).  Not measured in this run: returned with its source file."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None, None
     try:
         d = json.load(open(p))
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch"), p
+            return d.get("hbm_bytes_per_launch"), "profiles/pmc_traffic.json"
     except Exception:
         pass
     return None, None
+
+
+def launch_plan(steps: int, T: int) -> list[int]:
+    """Launch lengths covering exactly `steps` env steps in fused chunks of <= T steps."""
+    full, rem = divmod(int(steps), int(T))
+    return [T] * full + ([rem] if rem else [])
+
+
+def stagger_episodes(env, pdist_first: int) -> None:
+    """Spread the formations' episode phase (steps_since_reset) uniformly over the 1002-step
+    episode (simulate.py:111,231), as a long training run reaches when episodes desynchronise:
+    every timed window then contains the steady-state reset rate (1/1002 of the formations per
+    step, drawn in-kernel by Philox) instead of none or all of them."""
+    import torch
+    px, py, gx, gy, t = env.get_state()
+    F = t.numel()
+    ep = env.max_steps + 2
+    t = ((torch.arange(F, device=t.device, dtype=torch.int64) + pdist_first) % ep).to(torch.int32)
+    env.set_state(px, py, gx, gy, t)
 
 
 def main():
@@ -281,20 +320,25 @@ def main():
     ap.add_argument("--agents", type=int, default=5)
     ap.add_argument("--chunk", type=int, default=10)
     ap.add_argument("--reset-mode", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--episode-phase", default="staggered", choices=["staggered", "aligned"],
+                    help="staggered (philox only): formations spread over the episode, so every "
+                         "window includes resets; aligned: all start at t=0 like the reference")
     ap.add_argument("--no-goal", action="store_true")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--prewarm-ms", type=float, default=400.0,
+                    help="device-time pre-warm (clocks, first-touch of the buffers) before the "
+                         "--warmup steps; independent of --warmup, reported as warmup_ms")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
-    ap.add_argument("--event-group", type=int, default=5,
-                    help="HIP events bracket each run of this many consecutive rollout launches; "
-                         "avg launch duration = bracketed time / launches (includes the "
-                         "boundaries between them, so it is conservative)")
     ap.add_argument("--stats-every", type=int, default=10,
-                    help="reduce + all-reduce the episode stats every this many rollouts")
+                    help="reduce + all-reduce the episode stats every this many rollout launches "
+                         "(clamped to the timed launch count)")
     ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the secondary env-only lines (BASELINE configs[1] and [4])")
     args = ap.parse_args()
+    if args.steps < 1 or args.warmup < 0 or args.chunk < 1:
+        ap.error("need --steps >= 1, --warmup >= 0, --chunk >= 1")
 
     import torch
     import pkgload
@@ -322,74 +366,94 @@ def main():
     obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
     rew = torch.empty((T, A), dtype=torch.float32, device=dev)
     done = torch.empty((T, A), dtype=torch.bool, device=dev)
-    # stats pipeline: rollout k writes partials[k%2] on the main stream; a side stream reduces
-    # them (deterministic order) and all-reduces the two doubles over RCCL, overlapped with
-    # rollout k+1; rollout k+2 waits only for the side stream to have released partials[k%2].
+    # stats pipeline: a stats launch writes partials[s] on the main stream; a side stream reduces
+    # them (deterministic order) and all-reduces the two doubles over RCCL, overlapped with the
+    # next launches; the launch after next that reuses partials[s] waits for the side stream.
     partials = [torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=dev)
                 for _ in range(2)]
     reds = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
     released = [None, None]
-    main = torch.cuda.current_stream(dev)
+    main_s = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev)
     stats = pdist.StatsReducer(2, dev)
     env.reset_tensor()
+    phase = args.episode_phase if args.reset_mode == "philox" else "aligned"
+    if phase == "staggered":
+        stagger_episodes(env, first)
+    nstat = [0]
 
-    def chunk(k, ev=None, ev_end=None):
-        stat = not args.no_stats and (k + 1) % args.stats_every == 0
-        s = (k // args.stats_every) % 2
+    def launch(L, stat=False):
+        """One fused rollout of L steps (actions of slot nstat-parity; stats if `stat`)."""
+        s = nstat[0] % 2
         if stat and released[s] is not None:
-            main.wait_event(released[s])
-        if ev is not None:
-            ev[0].record(main)
-        env.rollout(acts[k % 2], obs, rew, done, partial=partials[s] if stat else None)
-        if ev_end is not None:
-            ev_end.record(main)
+            main_s.wait_event(released[s])
+        env.rollout(acts[s][:L], obs[:L], rew[:L], done[:L], partial=partials[s] if stat else None)
         if stat:
-            side.wait_stream(main)
+            side.wait_stream(main_s)
             with torch.cuda.stream(side):
                 stats.reserve()
                 env.reduce_partials(partials[s], reds[s])
                 stats.submit(reds[s])
                 released[s] = torch.cuda.Event()
                 released[s].record(side)
+            nstat[0] += 1
 
-    warm_chunks = max(1, -(-args.warmup // T))
-    n_chunks = max(args.stats_every, -(-args.steps // T))
-    steps = n_chunks * T
-    for k in range(warm_chunks):
-        chunk(k)
+    # 1) pre-warm by device time (clocks, first touch of the 2 GB rollout buffer, and the first
+    # launch of every kernel the timed region uses -- a kernel's first launch in a process costs
+    # milliseconds of host time, e.g. the stats reduction's), then 2) exactly --warmup steps,
+    # 3) exactly --steps timed steps.
+    pw_launches, pw_ms = 0, 0.0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    while pw_ms < args.prewarm_ms and pw_launches < 100000:
+        e0.record(main_s)
+        for j in range(5):
+            launch(T, stat=not args.no_stats and j == 4)
+        e1.record(main_s)
+        e1.synchronize()
+        pw_launches += 5
+        pw_ms += e0.elapsed_time(e1)
+    for L in launch_plan(args.warmup, T):
+        launch(L)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    G = max(1, args.event_group)
-    n_chunks = -(-n_chunks // G) * G
-    steps = n_chunks * T
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(n_chunks // G)]
+
+    plan = launch_plan(args.steps, T)
+    stat_every = max(1, min(args.stats_every, len(plan)))
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
     t0 = time.perf_counter()
-    for k in range(n_chunks):
-        g = evs[k // G]
-        chunk(k, g if k % G == 0 else None, g[1] if k % G == G - 1 else None)
+    evs[0].record(main_s)
+    for k, L in enumerate(plan):
+        launch(L, stat=not args.no_stats and (k + 1) % stat_every == 0)
+        evs[k + 1].record(main_s)
+    t_issued = time.perf_counter() - t0
     if not args.no_stats:
-        main.wait_stream(side)
+        main_s.wait_stream(side)
         tot = stats.result()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_avg_ms = sum(a.elapsed_time(b) for a, b in evs) / (len(evs) * G)
+    per_launch = [evs[k].elapsed_time(evs[k + 1]) for k in range(len(plan))]
+    kern_total_ms = sum(per_launch)
+    full = [ms for ms, L in zip(per_launch, plan) if L == T] or per_launch
+    kern_avg_ms = sum(full) / len(full)
     elapsed = pdist.max_over_ranks(elapsed, dev)
+    kern_total_ms = pdist.max_over_ranks(kern_total_ms, dev)
     kern_avg_ms = pdist.max_over_ranks(kern_avg_ms, dev)
 
+    steps = sum(plan)
     total_agents = total_formations * N
     value = total_agents * steps / elapsed
     bytes_launch = rollout_bytes_per_launch(A, N, D, T)
-    achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
+    bytes_timed = sum(rollout_bytes_per_launch(A, N, D, L) for L in plan)
+    achieved = bytes_timed / (kern_total_ms * 1e-3) / 1e9
     workload = (f"config3: {total_formations} formations x {N} agents "
                 f"({F} per GPU x {world}), fused {T}-step rollouts, {args.reset_mode} resets")
     traffic, tsrc = load_pmc_traffic(workload if world == 1 else "")
+    kname = env.rollout_kernel_name(T)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -397,30 +461,37 @@ def main():
             "unit": "agent-steps/s",
             "n_gpus": world,
             "steps": steps,
-            "warmup": warm_chunks * T,
+            "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: U(-1,1) fp32 actions resident in HBM, random-init formations",
+            "warmup_launches": pw_launches,
+            "warmup_ms": pw_ms,
+            "host_issue_ms": t_issued * 1e3,
             "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
+                       "episode_phase": phase, "timed_launches": plan,
                        "parallelism": f"formation-shard dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel": "k_rollout_wave (fenv_rollout)",
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": f"{kname} (fenv_rollout)",
                          "algorithmic_bytes_per_launch": bytes_launch,
-                         "avg_kernel_ms": kern_avg_ms, "launches": n_chunks,
-                         "launches_per_event_pair": G},
+                         "algorithmic_bytes_timed": bytes_timed,
+                         "avg_kernel_ms": kern_avg_ms, "kernel_ms_timed": kern_total_ms,
+                         "launches": len(plan),
+                         "launch_ms_min": min(per_launch), "launch_ms_max": max(per_launch),
+                         "timing": "HIP events on the launch stream at every launch boundary"},
         }
         if not args.no_stats:
             t = tot.cpu().tolist()
-            out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * T),
+            out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * plan[-1]),
                                     "agent_dones_sampled_rollout": t[1],
-                                    "every_rollouts": args.stats_every}
+                                    "every_launches": stat_every}
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
         if world == 1 and not args.no_policy:

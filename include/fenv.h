@@ -102,14 +102,24 @@ int fenv_rollout_random(fenv_t *env, int32_t T, uint64_t act_seed, uint64_t step
 /* Number of float2 partial records fenv_rollout writes (see fenv_rollout; independent of T). */
 int64_t fenv_partial_count(const fenv_t *env);
 
+/* Diagnostic (host only): name of the kernel fenv_rollout launches for a T-step launch of this
+ * env (for matching rocprofv3 kernel traces to bench lines). */
+const char *fenv_rollout_kernel(const fenv_t *env, int32_t T);
+
 /* Deterministic fixed-order reduction of `count` partial records into out[2] (double, device):
  * {sum of rewards, sum of agent-dones}. */
 int fenv_reduce_partials(const float *partial, int64_t count, double *out, void *stream);
 
-/* compute_metrics (simulate.py:238-254) per formation on the current state, plus the
- * per-formation mean reward logged at vectorized_env.py:80-81 (rew [A] may be NULL -> 0):
- * out [F][4] f32 = {avg_dist_to_goal, ave_dist_to_neighbor, std_dist_to_neighbor (unbiased,
- * NaN when N == 1), mean reward}.  sums (may be NULL) [4] double = sums of those over F. */
+/* Per-formation statistics the reference logs to wandb (rew [A] may be NULL -> 0), out [F][8] f32:
+ *   0 avg_dist_to_goal, 1 ave_dist_to_neighbor, 2 std_dist_to_neighbor (unbiased, NaN when
+ *     N == 1): compute_metrics (simulate.py:238-254) on the current (post-reset) state;
+ *   3 mean reward (vectorized_env.py:80-81);
+ *   4 close_to_goal_reward, 5 reward_dist, 6 reward_right_neighbor, 7 reward_left_neighbor:
+ *     means over the formation's agents of compute_reward_and_done's components
+ *     (simulate.py:183-208) for the state the env's latest step scored -- the terminal
+ *     (pre-reset) state of a formation that step reset; after fenv_reset / fenv_set_state,
+ *     of the current state.
+ * Means are summed in agent order in double.  sums (may be NULL) [8] double = column sums over F. */
 int fenv_metrics(fenv_t *env, const float *rew, float *out, double *sums, void *stream);
 
 /* State access (device buffers): px,py [A], gx,gy [F], t [F] = steps_since_reset.
@@ -145,11 +155,13 @@ float fenv_desired_neighbor_dist(int32_t num_agents);
  *   vf2.b[64] act.W[2][64] act.b[2] val.W[1][64] val.b[1] log_std[2]
  * obs [B][D]; outputs (each may be NULL): mu [B][2], value [B], action [B][2] (unclipped
  * sample, or mu if deterministic), logp [B], clipped [B][2].  eps ~ N(0,1) from Philox keyed
- * by (seed, counter offset `offset`, row). */
+ * by seed with counter (row0 + row, offset): pass row0 = the global index of row 0 (a shard's
+ * first agent) so that sharded and unsharded batches draw the same noise per agent. */
 int policy_param_count(int32_t obs_dim);
 int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B,
-                   float *mu, float *value, float *action, float *logp, float *clipped,
-                   uint64_t seed, uint64_t offset, int32_t deterministic, void *stream);
+                   int64_t row0, float *mu, float *value, float *action, float *logp,
+                   float *clipped, uint64_t seed, uint64_t offset, int32_t deterministic,
+                   void *stream);
 
 /* SB3 RolloutBuffer.compute_returns_and_advantage (GAE) over [T][A] device buffers:
  * rew, values f32, episode_starts u8 (1 where step k began an episode), last_values [A] f32
@@ -184,7 +196,9 @@ typedef struct fenv_rollout_bufs {
  * launch -- per step the policy forward (as policy_forward with seed and counter offset+k) and
  * the env step with the clipped action (as fenv_step), then the value of the final observation
  * -- followed by one GAE launch (as rollout_gae) when advantage/ret are given.  Observation 0 is the env's
- * current observation.  Results are bit-identical to the unfused calls.  Formation sizes
+ * current observation.  The noise of agent a is keyed by its global index (first_formation * N
+ * + a), as policy_forward with row0 = first_formation * N, so shards of one batch draw what the
+ * unsharded batch draws.  Results are bit-identical to the unfused calls.  Formation sizes
  * 1 <= N <= 64 (larger formations: policy_forward + fenv_step).  In FENV_RESET_MT19937 mode a
  * launch may contain at most one reset event (T <= max_steps + 2). */
 int fenv_policy_rollout(fenv_t *env, const float *params, int32_t T, uint64_t seed,

@@ -40,6 +40,7 @@ SIGNATURES = {
     "fenv_rollout": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
     "fenv_rollout_random": (_I32, [_P, _I32, _U64, _U64, _P, _P, _P, _P, _P, _P]),
     "fenv_partial_count": (_I64, [_P]),
+    "fenv_rollout_kernel": (ctypes.c_char_p, [_P, _I32]),
     "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
     "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),
     "fenv_get_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
@@ -48,7 +49,8 @@ SIGNATURES = {
     "fenv_desired_neighbor_dist": (ctypes.c_float, [_I32]),
     "fenv_fp_probe": (_I32, [_I32, _P, _P, _P, _I64, _P]),
     "policy_param_count": (_I32, [_I32]),
-    "policy_forward": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _U64, _U64, _I32, _P]),
+    "policy_forward": (_I32, [_P, _I32, _P, _I64, _I64, _P, _P, _P, _P, _P, _U64, _U64, _I32,
+                              _P]),
     "rollout_gae": (_I32, [_P, _P, _P, _P, _P, _I32, _I64, ctypes.c_float, ctypes.c_float, _P, _P,
                            _P]),
     "fenv_policy_rollout": (_I32, [_P, _P, _I32, _U64, _U64, _I32, ctypes.c_float,

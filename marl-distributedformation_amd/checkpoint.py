@@ -84,6 +84,69 @@ def optimizer_state_from_flat(shapes: list[tuple[str, tuple]], opt_state: dict) 
     return {"state": state, "param_groups": [g]}
 
 
+def optimizer_state_to_flat(shapes: list[tuple[str, tuple]], opt_state: dict | None,
+                            device) -> dict | None:
+    """Inverse of :func:`optimizer_state_from_flat`: SB3's Adam state over the 13 policy tensors
+    -> {step, exp_avg, exp_avg_sq} over the flat parameter (None if the state is absent,
+    empty or does not match the policy's shapes)."""
+    if not opt_state or not isinstance(opt_state.get("state"), dict) or not opt_state["state"]:
+        return None
+    st = opt_state["state"]
+    total = 0
+    for _, shp in shapes:
+        n = 1
+        for s in shp:
+            n *= int(s)
+        total += n
+    avg = torch.zeros(total, dtype=torch.float32)
+    sq = torch.zeros(total, dtype=torch.float32)
+    offs, o = {}, 0
+    for name, shp in shapes:
+        n = 1
+        for s in shp:
+            n *= int(s)
+        offs[name] = (o, n, tuple(shp))
+        o += n
+    step = None
+    for i, name in enumerate(SB3_PARAM_ORDER):
+        e = st.get(i) if i in st else st.get(str(i))
+        if not isinstance(e, dict) or "exp_avg" not in e or "exp_avg_sq" not in e:
+            return None
+        a, n, shp = offs[name]
+        ea, es = torch.as_tensor(e["exp_avg"]), torch.as_tensor(e["exp_avg_sq"])
+        if tuple(ea.shape) != shp or tuple(es.shape) != shp:
+            return None
+        avg[a:a + n] = ea.reshape(-1).float()
+        sq[a:a + n] = es.reshape(-1).float()
+        step = torch.as_tensor(e.get("step", 0)).float().reshape(())
+    dev = torch.device(device)
+    return {"step": step.to(dev), "exp_avg": avg.to(dev), "exp_avg_sq": sq.to(dev)}
+
+
+def plain_hyperparameters(data: dict, config_cls) -> dict:
+    """The fields of dataclass ``config_cls`` found in an SB3 ``data`` dict, skipping values SB3
+    stored as cloudpickled objects (``{":type:": ..., ":serialized:": ...}``, e.g. the
+    clip_range / learning_rate schedules) and values whose type does not match the field."""
+    out = {}
+    for k, f in config_cls.__dataclass_fields__.items():
+        if k not in data:
+            continue
+        v = data[k]
+        if isinstance(v, dict):
+            continue
+        want = type(f.default)
+        if want is bool:
+            if isinstance(v, bool):
+                out[k] = v
+        elif want is int:
+            if isinstance(v, int) and not isinstance(v, bool):
+                out[k] = v
+        elif want is float:
+            if isinstance(v, (int, float)) and not isinstance(v, bool):
+                out[k] = float(v)
+    return out
+
+
 def save_sb3_zip(path: str, state_dict: dict, *, num_timesteps: int, data: dict | None = None,
                  optimizer_state: dict | None = None) -> str:
     """Write an SB3-layout model zip; returns ``path`` (".zip" appended if missing, as SB3)."""
@@ -96,7 +159,8 @@ def save_sb3_zip(path: str, state_dict: dict, *, num_timesteps: int, data: dict 
     d.update({"num_timesteps": int(num_timesteps), "_total_timesteps": int(num_timesteps)})
     d.update(data or {})
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    tmp = path + ".tmp"
+    # the partial file's name must not look like a checkpoint to latest_checkpoint's rule
+    tmp = os.path.join(os.path.dirname(os.path.abspath(path)), f".partial-{os.getpid()}.zip")
     with zipfile.ZipFile(tmp, "w") as z:
         z.writestr("data", json.dumps(d, indent=4, sort_keys=False))
         z.writestr("policy.pth", _tensor_bytes(_state_to_cpu(state_dict)))
@@ -111,17 +175,28 @@ def save_sb3_zip(path: str, state_dict: dict, *, num_timesteps: int, data: dict 
     return path
 
 
-def load_sb3_zip(path: str) -> tuple[dict, dict]:
-    """(policy state_dict on CPU, data dict) from an SB3 model zip -- ours or SB3's.
+def load_sb3_zip(path: str, with_optimizer: bool = False):
+    """(policy state_dict on CPU, data dict[, optimizer state dict or None]) from an SB3 model
+    zip -- ours or SB3's.
 
-    Only ``policy.pth`` is deserialised, with ``torch.load(weights_only=True)``; ``data`` is
-    parsed as JSON and pickled entries are left as their JSON stubs."""
+    ``policy.pth`` (and ``policy.optimizer.pth`` when asked) are deserialised with
+    ``torch.load(weights_only=True)`` only; ``data`` is parsed as JSON and pickled entries are
+    left as their JSON stubs.  An optimizer entry the safe loader refuses is reported as None."""
     with zipfile.ZipFile(path) as z:
         names = set(z.namelist())
         if "policy.pth" not in names:
             raise ValueError(f"{path}: no policy.pth (not an SB3 model zip)")
         sd = torch.load(io.BytesIO(z.read("policy.pth")), map_location="cpu", weights_only=True)
         data = json.loads(z.read("data").decode()) if "data" in names else {}
+        opt = None
+        if with_optimizer and "policy.optimizer.pth" in names:
+            try:
+                opt = torch.load(io.BytesIO(z.read("policy.optimizer.pth")), map_location="cpu",
+                                 weights_only=True)
+            except Exception:
+                opt = None
+    if with_optimizer:
+        return dict(sd), data, opt
     return dict(sd), data
 
 
@@ -133,7 +208,7 @@ def checkpoint_name(num_timesteps: int, prefix: str = "rl_model") -> str:
 def latest_checkpoint(directory: str) -> str:
     """The newest checkpoint in ``directory``, chosen as visualize_policy.py:33-34 does: among the
     files whose name contains "rl_model", the one with the largest ``int(name.split("_")[-2])``."""
-    files = [f for f in os.listdir(directory) if "rl_model" in f]
+    files = [f for f in os.listdir(directory) if "rl_model" in f and f.endswith(".zip")]
     if not files:
         raise FileNotFoundError(f"no rl_model_*_steps.zip in {directory}")
     return os.path.join(directory, max(files, key=lambda x: int(x.split("_")[-2].split(".")[0])))

@@ -50,10 +50,11 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
                                            int64_t a, int i, uint32_t ep_new, float &px,
                                            float &py, float &gx, float &gy) {
     if (MODE == FENV_RESET_MT19937) {
-        px = p.px[a];
-        py = p.py[a];
-        gx = p.gx[f];
-        gy = p.gy[f];
+        const int64_t A = c.F * (int64_t)c.N;
+        px = p.pend[a];
+        py = p.pend[A + a];
+        gx = p.pend[2 * A + f];
+        gy = p.pend[2 * A + c.F + f];
     } else {
         const uint64_t fg = (uint64_t)(c.f0 + f);
         const uint64_t ag = fg * (uint64_t)c.N + (uint64_t)i;
@@ -170,6 +171,13 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
     s.t += 1;
     did_reset = false;
     if (dn) {                                         // :113-116 auto-reset
+        // keep the terminal (post-clip, pre-reset) state: the step's logged reward components
+        // (simulate.py:183-208) describe it, not the freshly drawn one
+        // (indices laundered inside the branch: otherwise the compiler hoists these rarely used
+        // addresses out of the step loop into 4 loop-invariant VGPRs)
+        int64_t ta = a;
+        asm volatile("" : "+v"(ta));
+        p.term[ta] = make_float4(s.px, s.py, s.gx, s.gy);
         const uint32_t ep_new = s.ep + 1;
         draw_reset<MODE>(c, p, f, a, i, ep_new, s.px, s.py, s.gx, s.gy);
         s.t = 0;

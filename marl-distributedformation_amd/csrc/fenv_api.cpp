@@ -66,13 +66,24 @@ struct fenv {
     float *hpend = nullptr;  // pinned host staging for `pend`
     hipEvent_t pend_ev = nullptr;
     bool pend_ev_recorded = false;
+    float *term = nullptr;   // device: terminal (px, py, gx, gy)[A] of the latest done step
+    bool term_valid = false; // last state-changing call was a step (t == 0 <=> reset by it)
     float *lv_scratch = nullptr;  // last values for GAE when the caller passes none
     std::mt19937 mt;         // the reference's global stream (all formations of all shards)
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
 
     size_t pend_floats() const { return (size_t)(2 * A + 2 * c.F); }
     fenvk::DevPending pending() const {
-        return fenvk::DevPending{pend, pend + A, pend + 2 * A, pend + 2 * A + c.F};
+        return fenvk::DevPending{pend, reinterpret_cast<float4 *>(term)};
+    }
+
+    // A launch that may read the staged set waits (on the device) for its latest refill, which
+    // may have been issued on another stream; refills are issued on the stream of the launch
+    // that consumed the previous set, so they never overtake a reader.
+    int wait_pending(hipStream_t st) {
+        if (c.reset_mode == FENV_RESET_MT19937 && pend_ev_recorded)
+            FENV_HIP(hipStreamWaitEvent(st, pend_ev, 0));
+        return FENV_OK;
     }
 
     // Draw the next reset set of the global stream; keep this shard's part; stage it to HBM.
@@ -94,8 +105,11 @@ struct fenv {
 
     // Apply a reset to every formation (pending set or Philox) and optionally write obs.
     int apply_reset(float *obs, hipStream_t st) {
+        int rc = wait_pending(st);
+        if (rc) return rc;
         FENV_HIP(fenvk::launch_reset_observe(c, s, pending(), D, true, obs, st));
         t_common = 0;
+        term_valid = false;
         return gen_pending(st);
     }
 
@@ -177,6 +191,10 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     e->s.ep = reinterpret_cast<uint32_t *>(e->s.t + F);
     he = hipMemset(state, 0, bytes);
     if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipMemset(state) failed"));
+    he = hipMalloc(&e->term, 4 * A * sizeof(float));
+    if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(terminal state) failed"));
+    he = hipMemset(e->term, 0, 4 * A * sizeof(float));
+    if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipMemset(terminal state) failed"));
     if (reset_mode == FENV_RESET_MT19937) {
         he = hipMalloc(&e->pend, e->pend_floats() * sizeof(float));
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
@@ -205,6 +223,7 @@ int fenv_destroy(fenv_t *e) {
     if (e->hpend) (void)hipHostFree(e->hpend);
     if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
     if (e->lv_scratch) (void)hipFree(e->lv_scratch);
+    if (e->term) (void)hipFree(e->term);
     delete e;
     return FENV_OK;
 }
@@ -223,6 +242,10 @@ int fenv_info(const fenv_t *e, int64_t *o) {
 }
 
 int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::rollout_group_count(e->c) : -1; }
+
+const char *fenv_rollout_kernel(const fenv_t *e, int32_t T) {
+    return e ? fenvk::rollout_kernel_name(e->c, T) : "";
+}
 
 int fenv_reset(fenv_t *e, float *obs, void *stream) {
     if (!e) return fail(FENV_EINVAL, "fenv_reset: NULL handle");
@@ -246,6 +269,11 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
     hipStream_t st = as_stream(stream);
     const int64_t A = e->A, D = e->D;
     int64_t k0 = 0;
+    if (T > 0) {
+        int rc = e->wait_pending(st);
+        if (rc) return rc;
+        e->term_valid = true;
+    }
     while (k0 < T) {
         int64_t L = T - k0;
         bool event = false;
@@ -313,7 +341,8 @@ int fenv_reduce_partials(const float *partial, int64_t count, double *out, void 
 int fenv_metrics(fenv_t *e, const float *rew, float *out, double *sums, void *stream) {
     if (!e || !out) return fail(FENV_EINVAL, "fenv_metrics: NULL argument");
     FENV_HIP(hipSetDevice(e->device));
-    FENV_HIP(fenvk::launch_metrics(e->c, e->s, rew, out, sums, nullptr, as_stream(stream)));
+    FENV_HIP(fenvk::launch_metrics(e->c, e->s, e->pending(), e->term_valid, rew, out, sums,
+                                   as_stream(stream)));
     return FENV_OK;
 }
 
@@ -355,6 +384,7 @@ int fenv_set_state(fenv_t *e, const float *px, const float *py, const float *gx,
     FENV_HIP(hipMemcpyAsync(e->s.gy, gy, F * 4, hipMemcpyDeviceToDevice, st));
     FENV_HIP(hipMemcpyAsync(e->s.t, t, F * 4, hipMemcpyDeviceToDevice, st));
     e->t_common = tc;
+    e->term_valid = false;
     return FENV_OK;
 }
 
@@ -387,14 +417,15 @@ int policy_param_count(int32_t obs_dim) {
     return 2 * (obs_dim * 64 + 64 + 64 * 64 + 64) + 130 + 65 + 2;
 }
 
-int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B, float *mu,
-                   float *value, float *action, float *logp, float *clipped, uint64_t seed,
-                   uint64_t offset, int32_t deterministic, void *stream) {
-    if (!params || !obs || B < 0 || (obs_dim != 6 && obs_dim != 8))
+int policy_forward(const float *params, int32_t obs_dim, const float *obs, int64_t B,
+                   int64_t row0, float *mu, float *value, float *action, float *logp,
+                   float *clipped, uint64_t seed, uint64_t offset, int32_t deterministic,
+                   void *stream) {
+    if (!params || !obs || B < 0 || row0 < 0 || (obs_dim != 6 && obs_dim != 8))
         return fail(FENV_EINVAL, "policy_forward: bad arguments (obs_dim must be 6 or 8)");
     if (B == 0) return FENV_OK;
-    FENV_HIP(fenvk::launch_policy_forward(params, obs_dim, obs, B, mu, value, action, logp, clipped,
-                                         seed, offset, deterministic, as_stream(stream)));
+    FENV_HIP(fenvk::launch_policy_forward(params, obs_dim, obs, B, row0, mu, value, action, logp,
+                                         clipped, seed, offset, deterministic, as_stream(stream)));
     return FENV_OK;
 }
 
@@ -427,6 +458,9 @@ int fenv_policy_rollout(fenv_t *e, const float *params, int32_t T, uint64_t seed
                                          "launch (T > max_steps + 2) in MT19937 mode");
         }
     }
+    int rc0 = e->wait_pending(st);
+    if (rc0) return rc0;
+    e->term_valid = true;
     const bool gae = b.advantage != nullptr;
     fenvk::PRArgs g{};
     g.b = b;

@@ -18,9 +18,15 @@ struct DevState {
     uint32_t *ep;    // [F]  episode counter (Philox reset key; not in the reference)
 };
 
-// Host-staged next reset draw set (FENV_RESET_MT19937 mode), same layout as DevState.
+// Reset-side buffers: the host-staged next reset draw set (FENV_RESET_MT19937 mode, same layout
+// as DevState) and the terminal (pre-reset, post-clip) state of the formations reset by their
+// latest done step, which compute_reward_and_done's logged components (simulate.py:183-208) are
+// taken from on a done step (written only on done steps; read by the metrics kernel).
+// Two kernel arguments instead of eight (the step kernels' SGPR budget).
 struct DevPending {
-    const float *px, *py, *gx, *gy;
+    const float *pend;  // staged draw set px[A] py[A] gx[F] gy[F] (NULL in Philox mode)
+    float4 *term;       // terminal (px, py, gx, gy)[A] (the goal repeated per agent: one
+                        // store, one index)
 };
 
 struct Consts {
@@ -56,15 +62,20 @@ hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &
                           const ActGen *gen = nullptr);
 hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPending &p,
                                 int32_t D, bool do_reset, float *obs, hipStream_t st);
-hipError_t launch_metrics(const Consts &c, const DevState &s, const float *rew, float *out,
-                          double *sums, double *scratch, hipStream_t st);
+// kMetricCols columns per formation (include/fenv.h fenv_metrics); `terminal`: formations with
+// steps_since_reset == 0 take their reward components from the terminal state (the env's last
+// state-changing call was a step, so t == 0 means "reset by that step").
+constexpr int kMetricCols = 8;
+hipError_t launch_metrics(const Consts &c, const DevState &s, const DevPending &p, bool terminal,
+                          const float *rew, float *out, double *sums, hipStream_t st);
+const char *rollout_kernel_name(const Consts &c, int32_t T);
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st);
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,
                            hipStream_t st);
 
 hipError_t launch_policy_forward(const float *params, int32_t D, const float *obs, int64_t B,
-                                 float *mu, float *value, float *action, float *logp,
+                                 int64_t row0, float *mu, float *value, float *action, float *logp,
                                  float *clipped, uint64_t seed, uint64_t offset,
                                  int32_t deterministic, hipStream_t st);
 

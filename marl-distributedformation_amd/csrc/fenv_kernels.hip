@@ -352,186 +352,14 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     }
 }
 
-// ---------------------------------------------------------------- workgroup-staged rollout (N <= 64)
-// Compute mapping of rollout_body (a wave holds fpw whole formations, lane = agent, ring
-// exchanges are wave shuffles, state in registers for the T steps); memory traffic per
-// WORKGROUP: kRW waves cover one contiguous agent slice whose actions come in and whose
-// obs / reward / done rows go out through LDS as contiguous full-width accesses, one barrier per
-// step (double-buffered).  At N = 5 or 10 a slice is 480 agents = whole 128-B lines of every
-// stream, where per-wave 60-agent rows straddle lines (tools/ubench_hbm.hip 'wgstage 480').
-#ifndef FENV_RW_OCC
-#define FENV_RW_OCC
-#endif
+// Workgroup-staged A/B variant (k_rollout_wg): source in tools/ab/k_rollout_wg.inc, compiled
+// in only with -DFENV_RW=1 (not in the product library).
 #ifndef FENV_RW
-#define FENV_RW 0  // 1: use k_rollout_wg for N <= 64 (A/B against k_rollout_wave)
+#define FENV_RW 0
 #endif
-#ifndef FENV_RW_K
-#define FENV_RW_K 8
+#if FENV_RW
+#include "../../tools/ab/k_rollout_wg.inc"
 #endif
-#ifndef FENV_RW_OBSBUF
-#define FENV_RW_OBSBUF 2  // 1: one obs stage + a second barrier per step (less LDS, more WGs/CU)
-#endif
-constexpr int kRW = FENV_RW_K;
-constexpr int kRWA = 64 * kRW;
-constexpr int kOB = FENV_RW_OBSBUF;
-
-struct RWLds {  // dynamic LDS layout, in floats
-    static constexpr int act = 0;                       // [2][kRWA] float2
-    static constexpr int rew = act + 2 * 2 * kRWA;      // [2][kRWA] float
-    static constexpr int done = rew + 2 * kRWA;         // [2][kRWA] uint8
-    static constexpr int red = done + 2 * (kRWA / 4);   // [kRW] float2
-    static constexpr int obs = red + 2 * kRW;           // [2][kRWA * D] float
-    static constexpr size_t bytes(int D) { return (size_t)(obs + kOB * kRWA * D) * sizeof(float); }
-};
-
-template <int D, int MODE>
-__global__ __launch_bounds__(64 * kRW) FENV_RW_OCC void k_rollout_wg(Consts c, DevState st,
-                                                                     DevPending p, int32_t T,
-                                                                     const float2 *__restrict__ act,
-                                                                     float *__restrict__ obs,
-                                                                     float *__restrict__ rew,
-                                                                     uint8_t *__restrict__ done,
-                                                                     float2 *__restrict__ partial,
-                                                                     bool accum) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float2 *s_act = reinterpret_cast<float2 *>(lds + RWLds::act);
-    float *s_rew = lds + RWLds::rew;
-    uint8_t *s_done = reinterpret_cast<uint8_t *>(lds + RWLds::done);
-    float2 *s_red = reinterpret_cast<float2 *>(lds + RWLds::red);
-    float *s_obs = lds + RWLds::obs;
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int N = c.N;
-    const int M = c.fpw * N;
-    const int fi = lane / N;
-    const int i = lane - fi * N;
-    const int64_t wave = (int64_t)blockIdx.x * kRW + w;
-    const int64_t f = wave * c.fpw + fi;
-    const bool active = fi < c.fpw && f < c.F;
-    const int64_t a = f * N + i;
-    const int li = w * M + lane;
-    const WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
-    const int64_t A = c.F * (int64_t)N;
-    const int64_t g0 = (int64_t)blockIdx.x * kRW * M;
-    const int nwg = (int)((A - g0) < (int64_t)kRW * M ? (A - g0) : (int64_t)kRW * M);
-    const bool a4 = ((A | g0 | (int64_t)nwg) & 1) == 0;  // slice loads as float4 (2 agents)
-    const int nld = a4 ? (nwg >> 1) : nwg;
-
-    Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
-    if (active) {
-        s.px = st.px[a];
-        s.py = st.py[a];
-        s.gx = st.gx[f];
-        s.gy = st.gy[f];
-        s.t = st.t[f];
-        s.ep = st.ep[f];
-    }
-    bool any_reset = false;
-    float rsum = 0.f, dsum = 0.f;
-    float4 nxt = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < nld) {
-        if (a4) nxt = reinterpret_cast<const float4 *>(act + g0)[tid];
-        else nxt = make_float4(act[g0 + tid].x, act[g0 + tid].y, 0.f, 0.f);
-        if (a4) reinterpret_cast<float4 *>(s_act)[tid] = nxt;
-        else s_act[tid] = make_float2(nxt.x, nxt.y);
-    }
-    __syncthreads();
-    for (int32_t k = 0; k < T; ++k) {
-        const int b = k & 1;
-        if (k + 1 < T && tid < nld) {  // next step's slice, in flight during this step
-            const float2 *src = act + (int64_t)(k + 1) * A + g0;
-            if (a4) nxt = reinterpret_cast<const float4 *>(src)[tid];
-            else nxt = make_float4(src[tid].x, src[tid].y, 0.f, 0.f);
-        }
-        const float2 ac = active ? s_act[b * kRWA + li] : make_float2(0.f, 0.f);
-        float rw;
-        bool dn, rs;
-        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
-        any_reset |= rs;
-        float o[8];
-        env_obs<D>(x, s, o);
-        if (kOB == 1 && k > 0) __syncthreads();  // previous step's obs writeback has drained
-        if (active) {
-            float *row = s_obs + (size_t)(kOB == 2 ? b : 0) * kRWA * D + li * D;
-            if (D == 8) {
-                reinterpret_cast<float4 *>(row)[0] = make_float4(o[0], o[1], o[2], o[3]);
-                reinterpret_cast<float4 *>(row)[1] = make_float4(o[4], o[5], o[6], o[7]);
-            } else {
-                reinterpret_cast<float2 *>(row)[0] = make_float2(o[0], o[1]);
-                reinterpret_cast<float2 *>(row)[1] = make_float2(o[2], o[3]);
-                reinterpret_cast<float2 *>(row)[2] = make_float2(o[4], o[5]);
-            }
-            s_rew[b * kRWA + li] = rw;
-            s_done[b * kRWA + li] = (uint8_t)dn;
-            rsum += rw;
-            dsum += dn ? 1.0f : 0.0f;
-        }
-        if (k + 1 < T && tid < nld) {
-            if (a4) reinterpret_cast<float4 *>(s_act + (b ^ 1) * kRWA)[tid] = nxt;
-            else s_act[(b ^ 1) * kRWA + tid] = make_float2(nxt.x, nxt.y);
-        }
-        __syncthreads();
-        const int64_t row0 = (int64_t)k * A + g0;
-        if (obs) {
-            const float *src = s_obs + (size_t)(kOB == 2 ? b : 0) * kRWA * D;
-            float *dst = obs + row0 * D;
-            const int nf = nwg * D;
-            if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && (nf & 3) == 0) {
-#pragma unroll 1
-                for (int q = tid; q < (nf >> 2); q += 64 * kRW)
-                    reinterpret_cast<float4 *>(dst)[q] = reinterpret_cast<const float4 *>(src)[q];
-            } else {
-#pragma unroll 1
-                for (int q = tid; q < (nf >> 1); q += 64 * kRW)
-                    reinterpret_cast<float2 *>(dst)[q] = reinterpret_cast<const float2 *>(src)[q];
-            }
-        }
-        if (rew) {
-            const float *src = s_rew + b * kRWA;
-            float *dst = rew + row0;
-            if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && (nwg & 3) == 0) {
-                if (tid < (nwg >> 2))
-                    reinterpret_cast<float4 *>(dst)[tid] = reinterpret_cast<const float4 *>(src)[tid];
-            } else {
-                if (tid < nwg) dst[tid] = src[tid];
-            }
-        }
-        if (done) {
-            const uint8_t *src = s_done + b * kRWA;
-            uint8_t *dst = done + row0;
-            if (((reinterpret_cast<uintptr_t>(dst) & 3) == 0) && (nwg & 3) == 0) {
-                if (tid < (nwg >> 2))
-                    reinterpret_cast<uint32_t *>(dst)[tid] = reinterpret_cast<const uint32_t *>(src)[tid];
-            } else {
-                if (tid < nwg) dst[tid] = src[tid];
-            }
-        }
-    }
-    if (active) {
-        st.px[a] = s.px;
-        st.py[a] = s.py;
-        if (i == 0) {
-            st.t[f] = s.t;
-            if (any_reset) {
-                st.gx[f] = s.gx;
-                st.gy[f] = s.gy;
-                st.ep[f] = s.ep;
-            }
-        }
-    }
-    if (partial) {
-        rsum = wave_sum(rsum);
-        dsum = wave_sum(dsum);
-        if (lane == 0) s_red[w] = make_float2(rsum, dsum);
-        __syncthreads();
-        if (tid == 0) {
-            float2 v = s_red[0];
-            for (int q = 1; q < kRW; ++q) v = make_float2(v.x + s_red[q].x, v.y + s_red[q].y);
-            if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
-            partial[blockIdx.x] = v;
-        }
-    }
-}
 
 // ---------------------------------------------------------------- reset + observe
 template <int D, int MODE, bool RESET, class X>
@@ -604,52 +432,89 @@ __global__ __launch_bounds__(1024) void k_reset_obs_block(Consts c, DevState st,
 }
 
 // ---------------------------------------------------------------- metrics (simulate.py:238-254)
-// Per formation: mean ||p - goal||, mean ||p_i - p_{i+1}||, its unbiased std, mean reward.
-// Each formation's values are staged in LDS and summed by its first lane in agent order
-// (deterministic), in double.
+// Per formation: mean ||p - goal||, mean ||p_i - p_{i+1}||, its unbiased std, mean reward
+// (compute_metrics on the current, post-reset state, simulate.py:117 + vectorized_env.py:80-81),
+// then the means of the four reward components compute_reward_and_done logs
+// (simulate.py:183-208: close-to-goal bonus, distance reward, right / left neighbour rewards) of
+// the state the last step scored -- the terminal state for a formation that step reset.  Each
+// formation's values are staged in LDS and summed by its first lane in agent order, in double.
+constexpr int kMS = 7;  // staged values per agent
 template <class X>
-__device__ __forceinline__ void metrics_body(const Consts &c, const DevState &st, const X &x,
+__device__ __forceinline__ void metrics_body(const Consts &c, const DevState &st,
+                                             const DevPending &p, bool terminal, const X &x,
                                              bool active, int64_t f, int64_t a, int i,
                                              const float *rew, float *stage, int base,
                                              float *out) {
     float px = 0.f, py = 0.f, gx = 0.f, gy = 0.f, r = 0.f;
+    bool term = false;
     if (active) {
         px = st.px[a];
         py = st.py[a];
         gx = st.gx[f];
         gy = st.gy[f];
         r = rew ? rew[a] : 0.f;
+        term = terminal && st.t[f] == 0;
+    }
+    float qx = px, qy = py, qgx = gx, qgy = gy;  // the state the last step's reward scored
+    if (term) {
+        const float4 tq = p.term[a];
+        qx = tq.x;
+        qy = tq.y;
+        qgx = tq.z;
+        qgy = tq.w;
     }
     float pnx, pny;
     x.a_next(px, py, pnx, pny);
     const float dg = norm2(px - gx, py - gy);
     const float dr = norm2(px - pnx, py - pny);
+    float qpx, qnx, qpy, qny;
+    x.d_pn(qx, qy, qpx, qnx, qpy, qny);
+    const float qg = norm2(qx - qgx, qy - qgy);                  // simulate.py:180
+    const float ctg = qg < 100.0f ? 10.0f : 0.0f;               // :183-187
+    const float rd = -0.1f * qg;                                // :191
+    const float rr = nb_reward(norm2(qx - qnx, qy - qny) - c.d_nb);  // :197, 202, 204
+    const float rl = nb_reward(norm2(qx - qpx, qy - qpy) - c.d_nb);  // :198, 203, 205
     const int N = c.N;
-    stage[3 * (base + i) + 0] = dg;
-    stage[3 * (base + i) + 1] = dr;
-    stage[3 * (base + i) + 2] = r;
+    float *sv = stage + kMS * (base + i);
+    sv[0] = dg;
+    sv[1] = dr;
+    sv[2] = r;
+    sv[3] = ctg;
+    sv[4] = rd;
+    sv[5] = rr;
+    sv[6] = rl;
     __syncthreads();
     if (active && i == 0) {
-        double sg = 0, sr = 0, sr2 = 0, rw = 0;
+        double sg = 0, sr = 0, sr2 = 0, rw = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0;
         for (int k = 0; k < N; ++k) {
-            const double d = stage[3 * (base + k) + 1];
-            sg += stage[3 * (base + k) + 0];
+            const float *v = stage + kMS * (base + k);
+            const double d = v[1];
+            sg += v[0];
             sr += d;
             sr2 += d * d;
-            rw += stage[3 * (base + k) + 2];
+            rw += v[2];
+            s3 += v[3];
+            s4 += v[4];
+            s5 += v[5];
+            s6 += v[6];
         }
         const double mr = sr / N;
-        out[f * 4 + 0] = (float)(sg / N);
-        out[f * 4 + 1] = (float)mr;
-        out[f * 4 + 2] = N > 1 ? (float)sqrt(fmax(0.0, (sr2 - N * mr * mr) / (N - 1)))
-                               : __builtin_nanf("");
-        out[f * 4 + 3] = (float)(rw / N);
+        float *o = out + f * kMetricCols;
+        o[0] = (float)(sg / N);
+        o[1] = (float)mr;
+        o[2] = N > 1 ? (float)sqrt(fmax(0.0, (sr2 - N * mr * mr) / (N - 1))) : __builtin_nanf("");
+        o[3] = (float)(rw / N);
+        o[4] = (float)(s3 / N);
+        o[5] = (float)(s4 / N);
+        o[6] = (float)(s5 / N);
+        o[7] = (float)(s6 / N);
     }
 }
 
-__global__ __launch_bounds__(256) void k_metrics_wave(Consts c, DevState st, const float *rew,
+__global__ __launch_bounds__(256) void k_metrics_wave(Consts c, DevState st, DevPending p,
+                                                      bool terminal, const float *rew,
                                                       float *out) {
-    __shared__ float stage[3 * 256];
+    __shared__ float stage[kMS * 256];
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int N = c.N;
@@ -658,27 +523,28 @@ __global__ __launch_bounds__(256) void k_metrics_wave(Consts c, DevState st, con
     const int64_t f = wave * c.fpw + fi;
     const bool active = fi < c.fpw && f < c.F;
     WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
-    metrics_body(c, st, x, active, f, f * N + i, i, rew, stage, (threadIdx.x & ~63) + fi * N,
-                 out);
+    metrics_body(c, st, p, terminal, x, active, f, f * N + i, i, rew, stage,
+                 (threadIdx.x & ~63) + fi * N, out);
 }
 
-__global__ __launch_bounds__(1024) void k_metrics_block(Consts c, DevState st, const float *rew,
+__global__ __launch_bounds__(1024) void k_metrics_block(Consts c, DevState st, DevPending p,
+                                                        bool terminal, const float *rew,
                                                         float *out) {
     __shared__ float lds[6 * kMaxN];
-    __shared__ float stage[3 * kMaxN];
+    __shared__ float stage[kMS * kMaxN];
     const int N = c.N;
     const int i = threadIdx.x;
     const int64_t f = blockIdx.x;
     const bool active = i < N;
     BlockX x{lds, i, active ? (i == 0 ? N - 1 : i - 1) : i, active ? (i == N - 1 ? 0 : i + 1) : i};
-    metrics_body(c, st, x, active, f, f * N + i, i, rew, stage, 0, out);
+    metrics_body(c, st, p, terminal, x, active, f, f * N + i, i, rew, stage, 0, out);
 }
 
 // ---------------------------------------------------------------- deterministic reductions
-// One workgroup; thread k sums elements k, k+1024, ... in double; then a fixed tree.
-template <int K, class T>
-__global__ __launch_bounds__(1024) void k_reduce_rows(const T *in, int64_t rows, double *out) {
-    __shared__ double red[K][1024];
+// One workgroup of NT threads; thread k sums elements k, k+NT, ... in double; then a fixed tree.
+template <int K, class T, int NT>
+__global__ __launch_bounds__(NT) void k_reduce_rows(const T *in, int64_t rows, double *out) {
+    __shared__ double red[K][NT];
     double acc[K][4];
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -686,19 +552,19 @@ __global__ __launch_bounds__(1024) void k_reduce_rows(const T *in, int64_t rows,
         for (int u = 0; u < 4; ++u) acc[j][u] = 0.0;
     // 4 independent rows in flight per thread per iteration (fixed assignment: deterministic)
     int64_t r = threadIdx.x;
-    for (; r + 3 * 1024 < rows; r += 4 * 1024) {
+    for (; r + 3 * NT < rows; r += 4 * NT) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int j = 0; j < K; ++j) acc[j][u] += (double)in[(r + u * 1024) * K + j];
+            for (int j = 0; j < K; ++j) acc[j][u] += (double)in[(r + u * NT) * K + j];
     }
-    for (; r < rows; r += 1024)
+    for (; r < rows; r += NT)
 #pragma unroll
         for (int j = 0; j < K; ++j) acc[j][0] += (double)in[r * K + j];
 #pragma unroll
     for (int j = 0; j < K; ++j) red[j][threadIdx.x] = (acc[j][0] + acc[j][1]) + (acc[j][2] + acc[j][3]);
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
+    for (int s = NT / 2; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) {
 #pragma unroll
             for (int j = 0; j < K; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + s];
@@ -754,7 +620,9 @@ static inline bool use_rs(const Consts &c, int32_t T) {
 }
 
 int64_t rollout_group_count(const Consts &c) {
-    if (FENV_RW && wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
+#if FENV_RW
+    if (wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
+#endif
     return group_count(c);
 }
 
@@ -786,11 +654,15 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
         return hipGetLastError();
     }
     const ActGen g0{};
-    if (FENV_RW && wave_path(c.N)) {
+#if FENV_RW
+    if (wave_path(c.N)) {
         hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
                            dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
                            accum);
-    } else if (use_rs(c, T)) {
+        return hipGetLastError();
+    }
+#endif
+    if (use_rs(c, T)) {
         hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
                            dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
                            a2, g0, obs, rew, done, p2, accum);
@@ -804,6 +676,14 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
                            accum);
     }
     return hipGetLastError();
+}
+
+const char *rollout_kernel_name(const Consts &c, int32_t T) {
+#if FENV_RW
+    if (wave_path(c.N)) return "k_rollout_wg";
+#endif
+    if (use_rs(c, T)) return "k_rollout_wave_rs";
+    return wave_path(c.N) ? "k_rollout_wave" : "k_rollout_block";
 }
 
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
@@ -849,25 +729,26 @@ hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPen
                   : reset_obs_d<6>(c, s, p, do_reset, obs, st);
 }
 
-hipError_t launch_metrics(const Consts &c, const DevState &s, const float *rew, float *out,
-                          double *sums, double *scratch, hipStream_t st) {
-    (void)scratch;
+hipError_t launch_metrics(const Consts &c, const DevState &s, const DevPending &p, bool terminal,
+                          const float *rew, float *out, double *sums, hipStream_t st) {
     if (wave_path(c.N)) {
         hipLaunchKernelGGL(k_metrics_wave, dim3((unsigned)group_count(c)), dim3(256), 0, st, c,
-                           s, rew, out);
+                           s, p, terminal, rew, out);
     } else {
         hipLaunchKernelGGL(k_metrics_block, dim3((unsigned)c.F), dim3(block_threads(c.N)), 0, st,
-                           c, s, rew, out);
+                           c, s, p, terminal, rew, out);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || sums == nullptr) return e;
-    hipLaunchKernelGGL((k_reduce_rows<4, float>), dim3(1), dim3(1024), 0, st, out, c.F, sums);
+    hipLaunchKernelGGL((k_reduce_rows<kMetricCols, float, 512>), dim3(1), dim3(512), 0, st, out,
+                       c.F, sums);
     return hipGetLastError();
 }
 
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st) {
-    hipLaunchKernelGGL((k_reduce_rows<2, float>), dim3(1), dim3(1024), 0, st, partial, count, out);
+    hipLaunchKernelGGL((k_reduce_rows<2, float, 1024>), dim3(1), dim3(1024), 0, st, partial, count,
+                       out);
     return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ namespace fenvk {
 // Persistent workgroups of 4 waves share one LDS weight image; each wave walks 32-agent tiles.
 __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params, int32_t D,
                                                const float *__restrict__ obs, int64_t B,
+                                               int64_t row0,
                                                float *__restrict__ mu_out,
                                                float *__restrict__ value_out,
                                                float *__restrict__ act_out,
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
         float o[8];
 #pragma unroll
         for (int col = 0; col < 8; ++col) o[col] = (valid && col < D) ? obs[row * D + col] : 0.0f;
-        const uint2 nb = deterministic ? make_uint2(0u, 0u) : policy_noise_bits(row, seed, offset);
+        const uint2 nb = deterministic ? make_uint2(0u, 0u) : policy_noise_bits(row0 + row, seed, offset);
         const PolicyLane r = policy_tile(lds, obs_operand(o, h), lane, nb, deterministic != 0,
                                          value_only);
         if (valid) {
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(256) void k_policy(const float *__restrict__ params
 }
 
 hipError_t launch_policy_forward(const float *params, int32_t D, const float *obs, int64_t B,
-                                 float *mu, float *value, float *action, float *logp,
+                                 int64_t row0, float *mu, float *value, float *action, float *logp,
                                  float *clipped, uint64_t seed, uint64_t offset,
                                  int32_t deterministic, hipStream_t st) {
     // Persistent grid sized to exactly the resident workgroups (no partial second round).
@@ -76,8 +77,8 @@ hipError_t launch_policy_forward(const float *params, int32_t D, const float *ob
         blocks = (tiles + 4 * rounds - 1) / (4 * rounds);
         if (blocks > resident) blocks = resident;
     }
-    hipLaunchKernelGGL(k_policy, dim3((unsigned)blocks), dim3(256), 0, st, params, D, obs, B, mu,
-                       value, action, logp, clipped, seed, offset, deterministic);
+    hipLaunchKernelGGL(k_policy, dim3((unsigned)blocks), dim3(256), 0, st, params, D, obs, B, row0,
+                       mu, value, action, logp, clipped, seed, offset, deterministic);
     return hipGetLastError();
 }
 

@@ -124,9 +124,10 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         tile_operands<D>(stage, j, h, bo);
         __builtin_amdgcn_wave_barrier();
         // Gaussian noise words: lane (j, h) draws them for agent j of tile h, so one Philox call
-        // per lane covers both tiles (each agent keeps its own (row, step) counter)
+        // per lane covers both tiles (each agent keeps its own (global row, step) counter)
         const uint2 mine = det ? make_uint2(0u, 0u)
-                               : policy_noise_bits(a_first + 32 * h + j, g.seed, g.offset + k);
+                               : policy_noise_bits(c.f0 * N + a_first + 32 * h + j, g.seed,
+                                                   g.offset + k);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             // one tile at a time, outputs parked in LDS at once

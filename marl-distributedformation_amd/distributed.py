@@ -1,7 +1,8 @@
-"""Formation sharding across ranks (one process per GPU) and the only collectives the env path
-needs: an all-reduce of episode statistics (and, once PPO runs on device, of the flat policy
-gradient).  The reference is single-process (no torch.distributed anywhere); this is
-new, per SURVEY §8(e): formations are independent, so env stepping needs no communication.
+"""Formation sharding across ranks (one process per GPU) and the only collectives the path
+needs: an all-reduce of episode statistics, one broadcast of the initial policy, and (PPO) one
+all-gather of every rank's rollout samples per update.  The reference is single-process (SURVEY
+§2: no torch.distributed anywhere); this is new, per SURVEY §8(e): formations are independent,
+so env stepping needs no communication.
 """
 from __future__ import annotations
 
@@ -106,13 +107,6 @@ def world_rank() -> tuple[int, int]:
     return 1, 0
 
 
-def sample_seed(seed: int, rank: int) -> int:
-    """Philox key of a rank's exploration noise.  The policy kernels key the noise by (local
-    row, step), so ranks sharing one seed would draw identical noise for their k-th agents;
-    rank r uses seed + r * 2^32 instead (rank 0 keeps the single-process stream)."""
-    return (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
-
-
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     """Replicate ``t`` from rank ``src`` in place (the policy parameters, once at start)."""
     world, _ = world_rank()
@@ -121,10 +115,36 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     return t
 
 
-def allreduce_mean_(t: torch.Tensor) -> torch.Tensor:
-    """In-place mean over ranks of one flat bucket (the 9,669-float policy gradient)."""
-    world, _ = world_rank()
-    if world > 1:
-        dist.all_reduce(t)
-        t.div_(world)
-    return t
+def shard_counts(total: int, world: int, scale: int = 1) -> list[int]:
+    """Rows owned by each rank: shard_range sizes x ``scale`` (agents per formation)."""
+    return [shard_range(total, r, world)[1] * int(scale) for r in range(world)]
+
+
+def gather_columns(local: torch.Tensor, counts: list[int], out: torch.Tensor | None = None):
+    """All-gather of a [T, A_r, C] tensor whose middle dimension is sharded contiguously over the
+    ranks (sizes ``counts``, which may differ by rank) -> [T, sum(counts), C], concatenated in rank
+    order along dim 1: exactly the unsharded tensor.  One collective (shards padded to the largest
+    count).  With world size 1 it is a copy."""
+    world, rank = world_rank()
+    T, Ar, C = local.shape
+    if Ar != counts[rank]:
+        raise ValueError(f"rank {rank}: local shard has {Ar} rows, counts say {counts[rank]}")
+    total = sum(counts)
+    if out is None:
+        out = torch.empty((T, total, C), dtype=local.dtype, device=local.device)
+    if world == 1:
+        out.copy_(local)
+        return out
+    amax = max(counts)
+    pad = local
+    if Ar != amax:
+        pad = torch.zeros((T, amax, C), dtype=local.dtype, device=local.device)
+        pad[:, :Ar].copy_(local)
+    parts = [torch.empty((T, amax, C), dtype=local.dtype, device=local.device)
+             for _ in range(world)]
+    dist.all_gather(parts, pad.contiguous())
+    o = 0
+    for r, n in enumerate(counts):
+        out[:, o:o + n].copy_(parts[r][:, :n])
+        o += n
+    return out

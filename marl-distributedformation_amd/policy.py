@@ -115,11 +115,12 @@ class MlpPolicy:
 
     # ---------------------------------------------------------------- forward
     def forward(self, obs: torch.Tensor, deterministic: bool = False, out: dict | None = None,
-                seed: int | None = None, offset: int | None = None) -> dict:
+                seed: int | None = None, offset: int | None = None, row0: int = 0) -> dict:
         """obs [B, D] float32 on the device -> dict(mu, value, action, log_prob, clipped).
 
         ``action`` is the unclipped sample (what SB3 stores in the rollout buffer); ``clipped``
-        is what collect_rollouts passes to env.step.  Each call advances the noise offset."""
+        is what collect_rollouts passes to env.step.  Each call advances the noise offset.
+        Row r's noise is keyed by the global row ``row0 + r`` (a shard passes its first agent)."""
         if obs.dim() != 2 or obs.shape[1] != self.obs_dim:
             raise ValueError(f"obs must be [B, {self.obs_dim}]")
         if obs.dtype != torch.float32 or obs.device != self.device:
@@ -127,6 +128,13 @@ class MlpPolicy:
         obs = obs.contiguous()
         B = obs.shape[0]
         dev = self.device
+        if out is not None:
+            for k, shp in (("mu", (B, 2)), ("value", (B,)), ("action", (B, 2)),
+                           ("log_prob", (B,)), ("clipped", (B, 2))):
+                t = out.get(k)
+                if t is not None and (t.device != dev or t.dtype != torch.float32
+                                      or tuple(t.shape) != shp or not t.is_contiguous()):
+                    raise ValueError(f"out[{k!r}] must be a contiguous float32 {shp} tensor on {dev}")
         if out is None:
             out = dict(mu=torch.empty((B, 2), device=dev), value=torch.empty(B, device=dev),
                        action=torch.empty((B, 2), device=dev), log_prob=torch.empty(B, device=dev),
@@ -136,7 +144,7 @@ class MlpPolicy:
             self._offset += 1
         s = self.sample_seed if seed is None else seed
         _lib.check(_lib.lib().policy_forward(
-            _lib.ptr(self.flat), self.obs_dim, _lib.ptr(obs), B, _lib.ptr(out.get("mu")),
+            _lib.ptr(self.flat), self.obs_dim, _lib.ptr(obs), B, int(row0), _lib.ptr(out.get("mu")),
             _lib.ptr(out.get("value")), _lib.ptr(out.get("action")), _lib.ptr(out.get("log_prob")),
             _lib.ptr(out.get("clipped")), int(s) & 0xFFFFFFFFFFFFFFFF, int(offset),
             int(bool(deterministic)), _lib.current_stream(dev)), "policy_forward")

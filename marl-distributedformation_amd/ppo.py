@@ -5,9 +5,14 @@ The reference's training run (vectorized_env.py:126-137) is SB3 PPO with ``n_ste
 ``batch_size=64``, ``gamma=0.99``, ``gae_lambda=0.95``, ``clip_range=0.2``, ``vf_coef=0.5``,
 ``max_grad_norm=0.5``, advantage normalisation, Adam eps 1e-5).  Rollouts come from
 :class:`rollout.RolloutCollector` (HIP kernels); the update differentiates a torch restatement of
-the same MLP over the SAME flat parameter buffer the kernel reads, so the gradient is one
-contiguous 9,669-float bucket: with several ranks it is all-reduced once per optimizer step
-(RCCL over xGMI), never per tensor.
+the same MLP over the SAME flat parameter buffer the kernel reads.
+
+Several ranks (one process per GPU, formations sharded): every rank collects its shard's rollout
+(policy noise keyed by the GLOBAL agent index, so the shards together draw exactly what the
+unsharded env draws), then ONE all-gather per update assembles the global [T, A_total] sample
+buffer in the unsharded order, and every rank runs the same update on it with the same
+permutations -- parameters and Adam state stay bitwise identical with no per-minibatch
+collective, and the result is the single-process update of the unsharded buffer.
 """
 from __future__ import annotations
 
@@ -83,6 +88,15 @@ def evaluate_actions(policy: MlpPolicy, flat: torch.Tensor, obs: torch.Tensor,
     return values, log_prob, entropy
 
 
+def epoch_permutations(n: int, n_epochs: int, gen: torch.Generator, device) -> torch.Tensor:
+    """[n_epochs, n] int64: one ``torch.randperm(n)`` per epoch from ``gen`` (SB3's
+    RolloutBuffer.get draws one permutation per epoch)."""
+    perm = torch.empty((int(n_epochs), int(n)), dtype=torch.long, device=device)
+    for e in range(int(n_epochs)):
+        perm[e].copy_(torch.randperm(int(n), device=device, generator=gen))
+    return perm
+
+
 class PPO:
     """Minimal on-device PPO: collect (HIP kernels) -> GAE (HIP) -> clipped-surrogate update."""
 
@@ -94,12 +108,26 @@ class PPO:
         self.policy = policy or MlpPolicy(env.obs_dim, device=env.device, seed=seed)
         self.buffer = RolloutBuffer(self.cfg.n_steps, env.num_envs, env.obs_dim, env.device,
                                     self.cfg.gamma, self.cfg.gae_lambda)
-        self.world, rank = pdist.world_rank()
+        self.world, self.rank = pdist.world_rank()
         # replicated weights: rank 0's, once (a loaded checkpoint or seed-identical init alike);
-        # per-rank noise streams (pdist.sample_seed)
+        # one noise seed for all ranks (the kernels key the noise by global agent index)
         pdist.broadcast_(self.policy.flat)
-        self.collector = RolloutCollector(env, self.policy, self.buffer,
-                                          seed=pdist.sample_seed(seed, rank))
+        self.collector = RolloutCollector(env, self.policy, self.buffer, seed=seed)
+        N = env.num_agents_per_formation
+        self.total_envs = env.num_envs
+        if self.world > 1:  # the env is this rank's shard of total_formations
+            self.total_envs = int(env.total_formations) * N
+            self.counts = pdist.shard_counts(int(env.total_formations), self.world, N)
+            if self.counts[self.rank] != env.num_envs:
+                raise ValueError("env shard does not match distributed.shard_range(total_formations, "
+                                 "rank, world)")
+        T, D = self.cfg.n_steps, env.obs_dim
+        # update samples [T, A_total, D + 5] = obs | action(2) | log_prob | advantage | return;
+        # with one rank they are views of the rollout buffer instead
+        self._gsamples = (torch.empty((T, self.total_envs, D + 5), dtype=torch.float32,
+                                      device=env.device) if self.world > 1 else None)
+        self._lsamples = (torch.empty((T, env.num_envs, D + 5), dtype=torch.float32,
+                                      device=env.device) if self.world > 1 else None)
         self.param = torch.nn.Parameter(self.policy.flat)  # shares storage with the kernel's
         self.param.grad = torch.zeros_like(self.param)     # static: graph replays write it
         # capturable: the step count lives on the device, so the update can be graph-captured
@@ -109,25 +137,53 @@ class PPO:
         self.stats: dict = {}
         # minibatch update as HIP graphs (one replay per minibatch instead of ~60 launches)
         self.use_graph = (self.param.device.type == "cuda") if use_graph is None else use_graph
-        n = self.buffer.n_steps * self.buffer.n_envs
+        n = self.buffer.n_steps * self.total_envs
         dev = self.param.device
         self._perm = torch.zeros(n, dtype=torch.long, device=dev)
         self._k = torch.zeros((), dtype=torch.long, device=dev)
         self._sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self._graphs = None
         # batch_size <= 64 (SB3's default 64): the whole update as one HIP kernel (ppo_update)
-        self.use_fused = ((self.param.device.type == "cuda" and self.world == 1
-                           and self.cfg.batch_size <= 64) if use_fused is None else use_fused)
+        self.use_fused = ((self.param.device.type == "cuda" and self.cfg.batch_size <= 64)
+                          if use_fused is None else use_fused)
 
     @property
     def num_timesteps(self) -> int:
-        return self.collector.num_timesteps * self.world
+        """Env steps of ALL ranks' agents so far (identical on every rank)."""
+        return self.collector.num_timesteps // self.env.num_envs * self.total_envs
+
+    # ---------------------------------------------------------------- samples
+    def gather_samples(self) -> None:
+        """World > 1: assemble the global update buffer (one all-gather, unsharded order)."""
+        if self.world == 1:
+            return
+        b, D = self.buffer, self.buffer.obs_dim
+        ls = self._lsamples
+        ls[..., :D].copy_(b.observations)
+        ls[..., D:D + 2].copy_(b.actions)
+        ls[..., D + 2].copy_(b.log_probs)
+        ls[..., D + 3].copy_(b.advantages)
+        ls[..., D + 4].copy_(b.returns)
+        pdist.gather_columns(ls, self.counts, out=self._gsamples)
+
+    def _flat(self):
+        """(obs, actions, old_log_prob, advantages, returns) over the update's n samples."""
+        b, D = self.buffer, self.buffer.obs_dim
+        if self.world == 1:
+            n = b.n_steps * b.n_envs
+            return (b.observations.reshape(n, D), b.actions.reshape(n, 2),
+                    b.log_probs.reshape(n), b.advantages.reshape(n), b.returns.reshape(n))
+        g = self._gsamples
+        n = g.shape[0] * g.shape[1]
+        g2 = g.view(n, D + 5)
+        return g2[:, :D], g2[:, D:D + 2], g2[:, D + 2], g2[:, D + 3], g2[:, D + 4]
+
+    def _permutations(self, n: int) -> torch.Tensor:
+        """SB3 RolloutBuffer.get's randperm, one per epoch, from this PPO's generator (seeded
+        alike on every rank, so all ranks draw the same permutations)."""
+        return epoch_permutations(n, self.cfg.n_epochs, self.gen, self.param.device)
 
     # ---------------------------------------------------------------- one minibatch
-    def _flat(self):
-        b, n = self.buffer, self.buffer.n_steps * self.buffer.n_envs
-        return (b.observations.reshape(n, b.obs_dim), b.actions.reshape(n, 2),
-                b.log_probs.reshape(n), b.advantages.reshape(n), b.returns.reshape(n))
 
     def _forward_backward(self, idx: torch.Tensor) -> None:
         """SB3 PPO.train inner loop up to loss.backward() for minibatch ``idx``; adds the
@@ -154,19 +210,14 @@ class PPO:
         torch.nn.utils.clip_grad_norm_([self.param], self.cfg.max_grad_norm)
         self.opt.step()
 
-    def _allreduce(self) -> None:
-        if self.world > 1:  # one flat 9,669-float bucket per optimizer step (RCCL)
-            pdist.allreduce_mean_(self.param.grad)
-
     def _eager_step(self, idx: torch.Tensor) -> None:
         self._forward_backward(idx)
-        self._allreduce()
         self._apply()
 
     def _capture(self, warm_idx: list) -> None:
-        """Record the full-minibatch step as HIP graph(s): [gather + forward + backward +
-        stats, k += 1] and [clip + Adam] (one graph when there is no all-reduce between).
-        The warm-up runs the first real minibatches eagerly on the capture stream."""
+        """Record the full-minibatch step as one HIP graph: gather + forward + backward + stats,
+        k += 1, clip + Adam.  The warm-up runs the first real minibatches eagerly on the capture
+        stream."""
         bs = self.cfg.batch_size
         # every tensor the graphs read must outlive them (a freed one's memory gets reused and
         # the replay would gather with garbage indices): attributes, not locals
@@ -187,18 +238,10 @@ class PPO:
                 self._k += 1
 
             g1 = torch.cuda.CUDAGraph()
-            if self.world > 1:
-                with torch.cuda.graph(g1, stream=s):
-                    fb()
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2, stream=s):
-                    self._apply()
-                self._graphs = (g1, g2)
-            else:
-                with torch.cuda.graph(g1, stream=s):
-                    fb()
-                    self._apply()
-                self._graphs = (g1, None)
+            with torch.cuda.graph(g1, stream=s):
+                fb()
+                self._apply()
+            self._graphs = (g1, None)
         torch.cuda.current_stream(self.param.device).wait_stream(s)
 
     def _train_fused(self) -> dict:
@@ -206,12 +249,11 @@ class PPO:
         same randperm per epoch, losses, clipping and Adam (state kept in ``self.opt``)."""
         from . import _lib
         c = self.cfg
-        n = self.buffer.n_steps * self.buffer.n_envs
+        obs, act, lp, adv, ret = (t.contiguous() for t in self._flat())
+        n = obs.shape[0]
         bs = min(int(c.batch_size), n)
         dev = self.param.device
-        perm = torch.empty((c.n_epochs, n), dtype=torch.long, device=dev)
-        for e in range(c.n_epochs):
-            perm[e].copy_(torch.randperm(n, device=dev, generator=self.gen))
+        perm = self._permutations(n)
         st = self.opt.state[self.param]
         if not st:  # torch's capturable-Adam state layout, created before the first step
             st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
@@ -222,7 +264,6 @@ class PPO:
                              max_grad_norm=c.max_grad_norm, lr=float(grp["lr"]),
                              beta1=float(grp["betas"][0]), beta2=float(grp["betas"][1]),
                              eps=float(grp["eps"]), normalize_advantage=int(c.normalize_advantage))
-        obs, act, lp, adv, ret = (t.contiguous() for t in self._flat())
         self._sums.zero_()
         _lib.check(_lib.lib().ppo_update(
             _lib.ptr(self.param), _lib.ptr(st["exp_avg"]), _lib.ptr(st["exp_avg_sq"]),
@@ -237,20 +278,23 @@ class PPO:
 
     def train(self) -> dict:
         """SB3 ``PPO.train``: n_epochs over shuffled minibatches of the rollout buffer (the same
-        randperm per epoch as ``RolloutBuffer.get``).  Full minibatches replay the captured
-        graph(s); a trailing partial minibatch runs eagerly.  Losses are summed on the device and
-        read once at the end."""
-        if self.use_fused and self.world == 1 and self.cfg.batch_size <= 64:
+        randperm per epoch as ``RolloutBuffer.get``) -- with several ranks, of the gathered global
+        buffer, identically on every rank.  Full minibatches replay the captured graph; a
+        trailing partial minibatch runs eagerly.  Losses are summed on the device and read once
+        at the end."""
+        self.gather_samples()
+        if self.use_fused and self.cfg.batch_size <= 64:
             return self._train_fused()
         c = self.cfg
-        n = self.buffer.n_steps * self.buffer.n_envs
+        n = self._flat()[0].shape[0]
         bs = min(int(c.batch_size), n)
         nfull, rem = divmod(n, bs)
         self._sums.zero_()
         steps = 0
         graph = self.use_graph and bs == c.batch_size and nfull > 0
-        for _ in range(c.n_epochs):
-            self._perm.copy_(torch.randperm(n, device=self.param.device, generator=self.gen))
+        perms = self._permutations(n)
+        for e in range(c.n_epochs):
+            self._perm.copy_(perms[e])
             self._k.zero_()
             first = 0
             if graph and self._graphs is None:
@@ -261,9 +305,6 @@ class PPO:
             for i in range(first, nfull):
                 if graph:
                     self._graphs[0].replay()
-                    if self._graphs[1] is not None:
-                        self._allreduce()
-                        self._graphs[1].replay()
                 else:
                     self._eager_step(self._perm[i * bs:(i + 1) * bs])
             if rem:
@@ -287,7 +328,7 @@ class PPO:
                 self.collector.collect()
             for cb in cbs:
                 if hasattr(cb, "on_steps") and rank == 0:
-                    cb.on_steps(self, self.cfg.n_steps, self.env.num_envs * self.world)
+                    cb.on_steps(self, self.cfg.n_steps, self.total_envs)
             self.train()
             stop = False
             for cb in cbs:
@@ -304,7 +345,7 @@ class PPO:
                 "n_epochs": c.n_epochs, "batch_size": c.batch_size, "gamma": c.gamma,
                 "gae_lambda": c.gae_lambda, "clip_range": c.clip_range, "vf_coef": c.vf_coef,
                 "max_grad_norm": c.max_grad_norm, "normalize_advantage": c.normalize_advantage,
-                "n_envs": self.env.num_envs * self.world, "seed": self.seed}
+                "n_envs": self.total_envs, "seed": self.seed}
 
     def save(self, path: str, num_timesteps: int | None = None) -> str:
         """SB3 ``model.save(path)``: an SB3-layout zip (checkpoint.py) with the policy's SB3
@@ -318,11 +359,20 @@ class PPO:
     def load(cls, path: str, env, cfg: PPOConfig | None = None, seed: int = 0) -> "PPO":
         """SB3 ``PPO.load(path, env)``: hyper-parameters from the zip's ``data`` (unless ``cfg``
         is given), policy weights from its ``policy.pth``."""
-        sd, data = ckpt.load_sb3_zip(path)
+        sd, data, opt_sd = ckpt.load_sb3_zip(path, with_optimizer=True)
         if cfg is None:
-            fields = PPOConfig.__dataclass_fields__
-            cfg = PPOConfig(**{k: data[k] for k in fields if k in data})
+            cfg = PPOConfig(**ckpt.plain_hyperparameters(data, PPOConfig))
         model = cls(env, cfg, seed=seed)
         model.policy.load_state_dict(sd)
-        model.loaded_num_timesteps = int(data.get("num_timesteps", 0))
+        # Adam moments and step count (SB3's per-tensor policy.optimizer.pth -> the flat state)
+        flat = ckpt.optimizer_state_to_flat(model.policy.param_shapes(), opt_sd, model.param.device)
+        if flat is not None:
+            st = model.opt.state[model.param]
+            st["step"] = flat["step"].to(torch.float32)
+            st["exp_avg"] = flat["exp_avg"]
+            st["exp_avg_sq"] = flat["exp_avg_sq"]
+        # timestep counter: SB3 keeps num_timesteps in ``data``
+        t = int(data.get("num_timesteps", 0)) if isinstance(data.get("num_timesteps", 0), int) else 0
+        model.loaded_num_timesteps = t
+        model.collector.num_timesteps = t // model.total_envs * env.num_envs
         return model

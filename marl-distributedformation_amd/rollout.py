@@ -138,11 +138,12 @@ class RolloutCollector:
         T = b.n_steps
         b.observations[0].copy_(self.last_obs)
         b.episode_starts[0].copy_(self.last_episode_starts)
+        row0 = self.env.first_formation * self.env.num_agents_per_formation  # global noise rows
         for k in range(T):
             self.policy.forward(b.observations[k], deterministic=deterministic,
                                 out=dict(mu=b.mu[k], value=b.values[k], action=b.actions[k],
                                          log_prob=b.log_probs[k], clipped=b.clipped[k]),
-                                seed=self.seed, offset=self.offset)
+                                seed=self.seed, offset=self.offset, row0=row0)
             self.offset += 1
             last = k == T - 1
             # the env is stepped with the clipped action (collect_rollouts np.clip)

@@ -64,9 +64,16 @@ class FormationView:
         return obs[self.index * N:(self.index + 1) * N].cpu()
 
     def compute_metrics(self) -> dict:
+        """simulate.py:238-254 (the values the reference logs when ``log``)."""
         m = self._env.metrics()[self.index].tolist()
         return {"avg_dist_to_goal": m[0], "ave_dist_to_neighbor": m[1],
                 "std_dist_to_neighbor": m[2]}
+
+    def reward_components(self) -> dict:
+        """The means compute_reward_and_done logs (simulate.py:183-208) for the last step."""
+        m = self._env.metrics()[self.index].tolist()
+        return dict(zip(("close_to_goal_reward", "reward_dist", "reward_right_neighbor",
+                         "reward_left_neighbor"), m[4:8]))
 
     def __repr__(self) -> str:
         return f"FormationView(index={self.index}, num_agents={self.num_agents})"

@@ -79,7 +79,21 @@ class _Infos(Sequence):
         return d
 
 
-class FormationEnv:
+def _vecenv_base():
+    """stable-baselines3's ``VecEnv`` when it is importable (the reference's base class,
+    vectorized_env.py:16), so ``PPO('MlpPolicy', env)`` accepts the env as a vectorised env;
+    ``object`` otherwise (SB3 is not installed in this image)."""
+    try:
+        from stable_baselines3.common.vec_env import VecEnv
+        return VecEnv
+    except Exception:
+        return object
+
+
+_BASE = _vecenv_base()
+
+
+class FormationEnv(_BASE):
     """Batched formation env on one HIP device (one shard of a multi-GPU batch)."""
 
     MAX_SPEED = 10  # vectorized_env.py:69
@@ -90,14 +104,20 @@ class FormationEnv:
                  first_formation: int = 0, total_formations: int | None = None):
         cfg = as_config(cfg)
         self.cfg = cfg
-        self.device = _lib.require_device(device if device is not None else cfg.get("device"))
         self.num_agents_per_formation = int(cfg.num_agents_per_formation)
         self.num_formation = int(cfg.num_formation)
         self.goal_in_obs = bool(cfg.goal_in_obs)
         self.obs_dim = 8 if self.goal_in_obs else 6          # vectorized_env.py:28-31
-        self.num_envs = self.num_agents_per_formation * self.num_formation  # :32
-        self.action_space = _make_box(-1, 1, (2,), np.float32)               # :34
-        self.observation_space = _make_box(-1, 1, (self.obs_dim,), np.float32)
+        num_envs = self.num_agents_per_formation * self.num_formation          # :32
+        action_space = _make_box(-1, 1, (2,), np.float32)                    # :34
+        observation_space = _make_box(-1, 1, (self.obs_dim,), np.float32)   # :35
+        if _BASE is not object:  # SB3 VecEnv base: the reference's super().__init__, :36
+            super().__init__(num_envs=num_envs, observation_space=observation_space,
+                             action_space=action_space)
+        self.num_envs = num_envs
+        self.action_space = action_space
+        self.observation_space = observation_space
+        self.device = _lib.require_device(device if device is not None else cfg.get("device"))
         # Q1: the reference never forwards cfg.share_reward_ratio (vectorized_env.py:43)
         self.share_reward_ratio = (float(cfg.share_reward_ratio) if honor_share_reward_ratio
                                    else 0.25)
@@ -277,6 +297,26 @@ class FormationEnv:
                    "fenv_observe")
         return self.obs_dev
 
+    def _check_out(self, name: str, t, shape: tuple, dtype) -> None:
+        """Caller-supplied output buffers go to the kernels as raw pointers: check them first."""
+        if t is None:
+            return
+        if not isinstance(t, torch.Tensor) or t.device != self.device:
+            raise ValueError(f"{name} must be a tensor on {self.device}")
+        if tuple(t.shape) != tuple(shape) or t.dtype != dtype or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)}, "
+                             f"got {t.dtype} {tuple(t.shape)}")
+
+    def _check_partial(self, partial) -> None:
+        if partial is None:
+            return
+        n = self.partial_count()
+        if (not isinstance(partial, torch.Tensor) or partial.device != self.device
+                or partial.dtype != torch.float32 or not partial.is_contiguous()
+                or partial.numel() < 2 * n):
+            raise ValueError(f"partial must be a contiguous float32 tensor on {self.device} with "
+                             f">= {2 * n} elements ({n} records)")
+
     def _check_act(self, act: torch.Tensor, lead: tuple) -> torch.Tensor:
         shape = lead + (self.num_envs, 2)
         if tuple(act.shape) != shape:
@@ -291,6 +331,10 @@ class FormationEnv:
         obs = self.obs_dev if obs is None else obs
         rew = self.rew_dev if rew is None else rew
         done = self.done_dev if done is None else done
+        A, D = self.num_envs, self.obs_dim
+        self._check_out("obs", obs, (A, D), torch.float32)
+        self._check_out("rew", rew, (A,), torch.float32)
+        self._check_out("done", done, (A,), torch.bool)
         _lib.check(_lib.lib().fenv_step(self._h, _lib.ptr(act), _lib.ptr(obs), _lib.ptr(rew),
                                         _lib.ptr(done), self._stream()), "fenv_step")
         return obs, rew, done
@@ -308,6 +352,10 @@ class FormationEnv:
             rew = torch.empty((T, A), dtype=torch.float32, device=dev)
         if done is None:
             done = torch.empty((T, A), dtype=torch.bool, device=dev)
+        self._check_out("obs", obs, (T, A, D), torch.float32)
+        self._check_out("rew", rew, (T, A), torch.float32)
+        self._check_out("done", done, (T, A), torch.bool)
+        self._check_partial(partial)
         _lib.check(_lib.lib().fenv_rollout(self._h, T, _lib.ptr(act), _lib.ptr(obs),
                                            _lib.ptr(rew), _lib.ptr(done), _lib.ptr(partial),
                                            self._stream()), "fenv_rollout")
@@ -329,9 +377,11 @@ class FormationEnv:
             rew = torch.empty((T, A), dtype=torch.float32, device=dev)
         if done is None:
             done = torch.empty((T, A), dtype=torch.bool, device=dev)
-        if act_out is not None and (tuple(act_out.shape) != (T, A, 2) or
-                                    act_out.dtype != torch.float32 or act_out.device != dev):
-            raise ValueError(f"act_out must be float32 [{T}, {A}, 2] on {dev}")
+        self._check_out("act_out", act_out, (T, A, 2), torch.float32)
+        self._check_out("obs", obs, (T, A, D), torch.float32)
+        self._check_out("rew", rew, (T, A), torch.float32)
+        self._check_out("done", done, (T, A), torch.bool)
+        self._check_partial(partial)
         _lib.check(_lib.lib().fenv_rollout_random(
             self._h, T, int(act_seed) & 0xFFFFFFFFFFFFFFFF, int(step_offset) & 0xFFFFFFFFFFFFFFFF,
             _lib.ptr(act_out), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done), _lib.ptr(partial),
@@ -348,12 +398,25 @@ class FormationEnv:
         last_value, advantage, ret; missing optional keys are skipped)."""
         if params.dtype != torch.float32 or params.device != self.device:
             raise TypeError(f"params must be float32 on {self.device}")
+        n = int(_lib.lib().policy_param_count(self.obs_dim))
+        if params.numel() != n or not params.is_contiguous():
+            raise ValueError(f"params must be a contiguous float32 vector of {n} elements")
+        T, A, D = int(T), self.num_envs, self.obs_dim
+        f32, u8 = torch.float32, torch.bool
+        shapes = dict(obs=((T, A, D), f32), last_obs=((A, D), f32), mu=((T, A, 2), f32),
+                      action=((T, A, 2), f32), clipped=((T, A, 2), f32), value=((T, A), f32),
+                      log_prob=((T, A), f32), reward=((T, A), f32),
+                      episode_start=((T, A), u8), done=((T, A), u8), last_done=((A,), u8),
+                      last_value=((A,), f32), advantage=((T, A), f32), ret=((T, A), f32))
+        unknown = set(bufs) - set(shapes)
+        if unknown:
+            raise ValueError(f"unknown rollout buffers {sorted(unknown)}")
         rb = _lib.RolloutBufs()
         for name, _ in _lib.RolloutBufs._fields_:
             t = bufs.get(name)
             if t is not None:
-                if t.device != self.device or not t.is_contiguous():
-                    raise ValueError(f"{name}: must be a contiguous tensor on {self.device}")
+                shp, dt = shapes[name]
+                self._check_out(name, t, shp, dt)
                 setattr(rb, name, t.data_ptr())
         _lib.check(_lib.lib().fenv_policy_rollout(
             self._h, _lib.ptr(params), int(T), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset),
@@ -365,16 +428,32 @@ class FormationEnv:
 
     def reduce_partials(self, partial: torch.Tensor, out: torch.Tensor | None = None):
         """Sum the per-wavefront {reward, done} records of :meth:`rollout` -> double[2]."""
+        self._check_partial(partial)
         if out is None:
             out = torch.empty(2, dtype=torch.float64, device=self.device)
+        self._check_out("out", out, (2,), torch.float64)
         _lib.check(_lib.lib().fenv_reduce_partials(_lib.ptr(partial), self.partial_count(),
                                                    _lib.ptr(out), self._stream()),
                    "fenv_reduce_partials")
         return out
 
+    METRIC_NAMES = ("avg_dist_to_goal", "ave_dist_to_neighbor", "std_dist_to_neighbor", "reward",
+                    "close_to_goal_reward", "reward_dist", "reward_right_neighbor",
+                    "reward_left_neighbor")
+
+    def rollout_kernel_name(self, T: int) -> str:
+        """The kernel fenv_rollout launches for a T-step launch of this env (diagnostic)."""
+        return _lib.lib().fenv_rollout_kernel(self._h, int(T)).decode()
+
     def metrics(self, rew: torch.Tensor | None = None, sums: torch.Tensor | None = None):
-        """simulate.py:238-254 per formation (+ mean reward): device tensor [F, 4]."""
-        out = torch.empty((self.num_formation, 4), dtype=torch.float32, device=self.device)
+        """Per-formation wandb statistics of the reference, device tensor [F, 8] (columns
+        METRIC_NAMES): compute_metrics (simulate.py:238-254) on the current state, the mean
+        reward (vectorized_env.py:80-81), and the means of compute_reward_and_done's logged
+        components (simulate.py:183-208) for the state the latest step scored.  ``sums``
+        (float64 [8], optional) receives the column sums over formations."""
+        self._check_out("rew", rew, (self.num_envs,), torch.float32)
+        self._check_out("sums", sums, (8,), torch.float64)
+        out = torch.empty((self.num_formation, 8), dtype=torch.float32, device=self.device)
         _lib.check(_lib.lib().fenv_metrics(self._h, _lib.ptr(rew), _lib.ptr(out), _lib.ptr(sums),
                                            self._stream()), "fenv_metrics")
         return out

@@ -152,7 +152,9 @@ class NumpyOracleEnv:
         self.p = np.zeros((self.F, self.N, 2), np.float32)
         self.g = np.zeros((self.F, 2), np.float32)
         self.t = np.zeros(self.F, np.int32)
+        self.comp = np.zeros((self.F, 4))
         self._reset_formations(np.arange(self.F))      # ctor draw set (simulate.py:61)
+        self.comp = self._components(self.p)
 
     # simulate.py:120-147, drawn in formation order
     def _reset_formations(self, idx: np.ndarray) -> None:
@@ -179,7 +181,27 @@ class NumpyOracleEnv:
 
     def reset(self) -> np.ndarray:
         self._reset_formations(np.arange(self.F))
+        self.comp = self._components(self.p)
         return self.observe()
+
+    def _components(self, p: np.ndarray) -> np.ndarray:
+        """Per-formation means (float64, agent order) of close_to_goal_reward, reward_dist,
+        reward_right_neighbor, reward_left_neighbor (simulate.py:183-208) for positions p."""
+        dg = norm2(p[..., 0] - self.g[:, None, 0], p[..., 1] - self.g[:, None, 1])
+        pr, pl = np.roll(p, -1, axis=1), np.roll(p, 1, axis=1)
+        dr = norm2(p[..., 0] - pr[..., 0], p[..., 1] - pr[..., 1]) - self.d_nb
+        dl = norm2(p[..., 0] - pl[..., 0], p[..., 1] - pl[..., 1]) - self.d_nb
+        parts = [np.where(dg < np.float32(100), np.float32(10), np.float32(0)),
+                 np.float32(-0.1) * dg,
+                 np.float32(-0.01) * np.where(dr < 0, dr * dr, dr),
+                 np.float32(-0.01) * np.where(dl < 0, dl * dl, dl)]
+        out = np.zeros((self.F, 4))
+        for k, v in enumerate(parts):
+            acc = np.zeros(self.F)
+            for i in range(self.N):  # agent order, as the C oracle and the kernel
+                acc += v[:, i].astype(np.float64)
+            out[:, k] = acc / self.N
+        return out
 
     def step(self, actions: np.ndarray):
         a = np.asarray(actions, np.float32).reshape(self.F, self.N, 2)
@@ -191,6 +213,7 @@ class NumpyOracleEnv:
         p[..., 1] = np.where(p[..., 1] < 0, np.float32(0),
                              np.where(p[..., 1] > np.float32(H), np.float32(H), p[..., 1]))
         self.p = p.astype(np.float32)
+        self.comp = self._components(self.p)
         dg = norm2(p[..., 0] - self.g[:, None, 0], p[..., 1] - self.g[:, None, 1])
         ctg = np.where(dg < np.float32(100), np.float32(10), np.float32(0))
         rd = np.float32(-0.1) * dg
@@ -218,7 +241,8 @@ class NumpyOracleEnv:
         dg = norm2(p[..., 0] - self.g[:, None, 0], p[..., 1] - self.g[:, None, 1]).astype(np.float64)
         pr = np.roll(p, -1, axis=1)
         dr = norm2(p[..., 0] - pr[..., 0], p[..., 1] - pr[..., 1]).astype(np.float64)
-        out = np.zeros((self.F, 4))
+        out = np.zeros((self.F, 8))
+        out[:, 4:] = self.comp
         out[:, 0] = dg.mean(1)
         out[:, 1] = dr.mean(1)
         out[:, 2] = dr.std(1, ddof=1) if self.N > 1 else np.nan
@@ -302,7 +326,9 @@ class COracleEnv:
                               _ptr(self.done))
 
     def metrics(self, rew: np.ndarray | None = None) -> np.ndarray:
-        out = np.zeros((self.F, 4), np.float64)
+        """[F, 8]: compute_metrics (3), mean reward, reward components of the last scored state
+        (see fenv_oracle.c orc_env_metrics)."""
+        out = np.zeros((self.F, 8), np.float64)
         r = None if rew is None else np.ascontiguousarray(rew, np.float32)
         self.lib.orc_env_metrics(self.h, None if r is None else _ptr(r), _ptr(out))
         return out

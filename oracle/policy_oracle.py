@@ -87,9 +87,10 @@ def _philox(ctr: np.ndarray, key: tuple[int, int]) -> np.ndarray:
     return c
 
 
-def philox_normals(B: int, seed: int, offset: int) -> np.ndarray:
-    """The kernel's N(0,1) noise [B, 2] (Box-Muller of Philox4x32-10 words), in float64."""
-    rows = np.arange(B, dtype=np.uint64)
+def philox_normals(B: int, seed: int, offset: int, row0: int = 0) -> np.ndarray:
+    """The kernel's N(0,1) noise [B, 2] (Box-Muller of Philox4x32-10 words) for global rows
+    row0 .. row0+B-1, in float64."""
+    rows = np.arange(row0, row0 + B, dtype=np.uint64)
     ctr = np.stack([rows & np.uint64(0xFFFFFFFF), rows >> np.uint64(32),
                     np.full(B, offset & 0xFFFFFFFF, np.uint64),
                     np.full(B, (offset >> 32) & 0xFFFFFFFF, np.uint64)], axis=1)

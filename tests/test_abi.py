@@ -8,6 +8,7 @@
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -86,7 +87,8 @@ def test_bad_arguments_rejected_without_device(flib):
     assert L.fenv_host_reset_draws(1, 0, 2, 1, 5, 5, None, None, None, None) == -1
     assert b"bad arguments" in L.fenv_last_error()
     assert L.fenv_reduce_partials(None, 1, None, None) == -1
-    assert L.policy_forward(None, 8, None, 1, None, None, None, None, None, 0, 0, 0, None) == -1
+    assert L.policy_forward(None, 8, None, 1, 0, None, None, None, None, None, 0, 0, 0,
+                            None) == -1
     assert L.policy_param_count(8) == 9669  # SURVEY §8(a) R10 (incl. log_std[2])
 
 
@@ -127,3 +129,69 @@ def test_ppo_update_validates_before_launch(flib):
     nul = list(args)
     nul[0] = None
     assert L.ppo_update(*nul) != 0
+
+
+SB3_STUB = r"""
+import abc, sys, types
+rec = {}
+class VecEnv(abc.ABC):
+    # SB3 2.x VecEnv: constructor arguments and abstract methods
+    def __init__(self, num_envs, observation_space, action_space):
+        rec.update(num_envs=num_envs, observation_space=observation_space,
+                   action_space=action_space)
+        self.num_envs = num_envs
+        self.observation_space = observation_space
+        self.action_space = action_space
+        try:
+            self.get_attr("render_modes")
+        except AttributeError:
+            rec["get_attr_raised"] = True
+    for _m in ("reset", "step_async", "step_wait", "close", "get_attr", "set_attr",
+               "env_method", "env_is_wrapped"):
+        locals()[_m] = abc.abstractmethod(lambda self, *a, **k: None)
+def mod(name, **kw):
+    m = types.ModuleType(name); m.__dict__.update(kw); sys.modules[name] = m
+mod("stable_baselines3"); mod("stable_baselines3.common")
+mod("stable_baselines3.common.vec_env", VecEnv=VecEnv)
+"""
+
+
+def test_formation_env_is_sb3_vecenv_when_sb3_importable():
+    """With an SB3 stand-in importable (the same sys.modules recipe gen_golden.py uses), the
+    env subclasses SB3's VecEnv and calls its __init__ with the reference's arguments
+    (vectorized_env.py:16, 36): num_envs = N * F and Box(-1, 1) spaces of shapes (D,) / (2,).
+    Runs in a subprocess so the stand-in does not leak into other tests.  Without a device the
+    constructor then fails loudly (no CPU path); GPU construction: tests/test_gpu_parity.py."""
+    code = SB3_STUB + r"""
+sys.path.insert(0, %r)
+import pkgload
+pkg = pkgload.load()
+from importlib import import_module
+ve = import_module(pkg.__name__ + ".vectorized_env")
+assert issubclass(ve.FormationEnv, VecEnv), ve.FormationEnv.__mro__
+assert not getattr(ve.FormationEnv, "__abstractmethods__", None)
+env = ve.FormationEnv.__new__(ve.FormationEnv)
+for m, args, exc in (("close", (), NotImplementedError), ("env_is_wrapped", (None,), NotImplementedError),
+                     ("get_attr", ("x",), AttributeError), ("set_attr", ("x", 1), NotImplementedError),
+                     ("env_method", ("x",), NotImplementedError), ("seed", (), NotImplementedError),
+                     ("step_async", (None,), NotImplementedError), ("step_wait", (), NotImplementedError)):
+    try:
+        getattr(env, m)(*args)
+    except exc:
+        pass
+    else:
+        raise AssertionError(m)
+try:
+    ve.FormationEnv({"num_formation": 7, "num_agents_per_formation": 5, "goal_in_obs": False})
+except RuntimeError as e:
+    assert "no HIP device" in str(e) or "HIP" in str(e), e
+import torch
+if not torch.cuda.is_available():
+    assert rec["num_envs"] == 35
+    assert tuple(rec["observation_space"].shape) == (6,) and tuple(rec["action_space"].shape) == (2,)
+    assert float(rec["action_space"].low.min()) == -1.0 and float(rec["action_space"].high.max()) == 1.0
+    assert rec["get_attr_raised"]
+print("ok")
+""" % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]

@@ -80,10 +80,56 @@ def test_optimizer_state_sliced_per_sb3_tensor(ck, shapes):
         assert torch.equal(ea, exp)
 
 
-def test_latest_checkpoint_rule(ck, tmp_path):
+def test_optimizer_state_roundtrip_to_flat(ck, shapes):
+    """SB3's per-tensor Adam state (as policy.optimizer.pth holds it) back onto the flat
+    parameter: the exact moments and step that were saved (PPO.load restores them)."""
+    n = sum(torch.Size(s).numel() for _, s in shapes)
+    flat = torch.nn.Parameter(torch.zeros(n))
+    opt = torch.optim.Adam([flat], lr=1e-3, eps=1e-5)
+    for k in range(3):
+        flat.grad = torch.randn(n, generator=torch.Generator().manual_seed(k))
+        opt.step()
+    sb3 = ck.optimizer_state_from_flat(shapes, opt.state_dict())
+    buf = io.BytesIO()
+    torch.save(sb3, buf)  # what save_sb3_zip writes; read back with the safe loader
+    sb3 = torch.load(io.BytesIO(buf.getvalue()), weights_only=True)
+    back = ck.optimizer_state_to_flat(shapes, sb3, "cpu")
+    st = opt.state_dict()["state"][0]
+    assert torch.equal(back["exp_avg"], st["exp_avg"])
+    assert torch.equal(back["exp_avg_sq"], st["exp_avg_sq"])
+    assert float(back["step"]) == 3.0
+    assert ck.optimizer_state_to_flat(shapes, None, "cpu") is None
+    assert ck.optimizer_state_to_flat(shapes, {"state": {}, "param_groups": []}, "cpu") is None
+    bad = {"state": {0: {"exp_avg": torch.zeros(3), "exp_avg_sq": torch.zeros(3), "step": 1}}}
+    assert ck.optimizer_state_to_flat(shapes, bad, "cpu") is None
+
+
+def test_sb3_pickled_hyperparameters_skipped(ck, pkg):
+    """SB3 stores clip_range / learning_rate as cloudpickled schedules ({":type:", ":serialized:"}
+    dicts in ``data``): PPO.load must not feed them to PPOConfig."""
+    from importlib import import_module
+    ppo = import_module(pkg.__name__ + ".ppo")
+    data = {"clip_range": {":type:": "<class 'function'>", ":serialized:": "gAWV..."},
+            "learning_rate": {":type:": "<class 'function'>", ":serialized:": "gAWV..."},
+            "n_steps": 10, "batch_size": 64, "gamma": 0.99, "ent_coef": 0.01,
+            "normalize_advantage": True, "n_epochs": "10", "vf_coef": True, "gae_lambda": 1}
+    got = ck.plain_hyperparameters(data, ppo.PPOConfig)
+    assert got == {"n_steps": 10, "batch_size": 64, "gamma": 0.99, "ent_coef": 0.01,
+                   "normalize_advantage": True, "gae_lambda": 1.0}
+    cfg = ppo.PPOConfig(**got)
+    assert cfg.clip_range == 0.2 and cfg.learning_rate == 1e-3
+
+
+def test_latest_checkpoint_rule(ck, shapes, tmp_path):
     for t in (20, 100, 3, 99):
         (tmp_path / ck.checkpoint_name(t)).write_bytes(b"")
     (tmp_path / "notes.txt").write_text("x")
+    # a partial file a crashed save could leave behind is never picked
+    (tmp_path / "rl_model_500_steps.zip.tmp").write_bytes(b"")
+    assert ck.latest_checkpoint(str(tmp_path)).endswith("rl_model_100_steps.zip")
+    # save_sb3_zip's own partial file does not look like a checkpoint
+    ck.save_sb3_zip(str(tmp_path / ck.checkpoint_name(7)), random_sd(shapes), num_timesteps=7)
+    assert not [f for f in os.listdir(tmp_path) if "partial" in f]
     assert ck.latest_checkpoint(str(tmp_path)).endswith("rl_model_100_steps.zip")
     (tmp_path / "empty").mkdir()
     with pytest.raises(FileNotFoundError):

@@ -1,5 +1,6 @@
 """Multi-process (gloo, world_size 2, CPU) coverage of the N>1 path: formation sharding, the
-sharded MT19937 reset stream and the stats all-reduce used by bench.py / training."""
+sharded MT19937 reset stream, the stats all-reduce used by bench.py / training, and PPO's
+once-per-update sample all-gather + shared epoch permutations (uneven shards)."""
 import os
 import socket
 
@@ -34,6 +35,11 @@ def test_shard_range_partitions(pkg):
         d.shard_range(10, 2, 2)
 
 
+def _global_samples(T, A, C):
+    """Deterministic stand-in for an unsharded [T, A, C] update buffer (distinct values)."""
+    return torch.arange(T * A * C, dtype=torch.float32).reshape(T, A, C) * 0.5 - 7.0
+
+
 def _worker(rank, world, port, root, q):
     import sys
     sys.path.insert(0, root)
@@ -66,15 +72,23 @@ def _worker(rank, world, port, root, q):
         red.submit(bufs[k % 2])
     out = red.result().clone()
     mx = d.max_over_ranks(float(rank) * 3.0)
-    # PPO's collectives: rank 0's parameters replicated once, gradient bucket averaged
+    # PPO's collectives: rank 0's parameters replicated once; per update ONE all-gather of the
+    # [T, A_r, D+5] samples of uneven shards (11 formations x 5 agents: 30 + 25 rows)
     params = torch.full((9669,), float(rank + 1))
     d.broadcast_(params)
-    grad = torch.arange(9669, dtype=torch.float32) * (rank + 1)
-    d.allreduce_mean_(grad)
-    seeds = [None] * world
-    dist.all_gather_object(seeds, d.sample_seed(12345, rank))
+    counts = d.shard_counts(total, world, N)
+    T, C = 3, 13
+    glob = _global_samples(T, total * N, C)
+    a0 = sum(counts[:rank])
+    local = glob[:, a0:a0 + counts[rank]].clone()
+    gathered = d.gather_columns(local, counts)
+    # the update's permutations: one randperm per epoch from a generator seeded alike
+    ppo = import_module(pkg.__name__ + ".ppo")
+    perms = ppo.epoch_permutations(T * total * N, 4, torch.Generator().manual_seed(7), "cpu")
+    got = [None] * world
+    dist.all_gather_object(got, (gathered.numpy().tobytes(), perms.numpy().tobytes()))
     if rank == 0:
-        q.put((parts, out.tolist(), mx, float(params.sum()), grad[:4].tolist(), seeds))
+        q.put((parts, out.tolist(), mx, float(params.sum()), counts, got))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -87,7 +101,7 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q)) for r in range(2)]
     for p in procs:
         p.start()
-    parts, out, mx, psum, g4, seeds = q.get(timeout=120)
+    parts, out, mx, psum, counts, got = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -105,5 +119,13 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     assert out == [float(0 + 4) + float(1 + 4), 2.0]
     assert mx == 3.0
     assert psum == 9669.0                        # rank 0's ones everywhere
-    assert g4 == [0.0, 1.5, 3.0, 4.5]            # mean of k and 2k
-    assert seeds[0] == 12345 and seeds[1] != seeds[0]  # rank 0 keeps the single-GPU stream
+    assert counts == [30, 25]                    # uneven shards (6 + 5 formations)
+    # both ranks gathered the same buffer, equal to the unsharded (world-1) one, and drew the
+    # same permutations as a world-1 run
+    want = _global_samples(3, total * N, 13).numpy().tobytes()
+    assert got[0][0] == want and got[1][0] == want
+    from importlib import import_module
+    import pkgload
+    ppo = import_module(pkgload.load().__name__ + ".ppo")
+    perms = ppo.epoch_permutations(3 * total * N, 4, torch.Generator().manual_seed(7), "cpu")
+    assert got[0][1] == got[1][1] == perms.numpy().tobytes()

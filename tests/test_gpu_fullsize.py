@@ -14,6 +14,7 @@ import pytest
 import torch
 
 from oracle import COracleEnv
+from tolerance import assert_rel_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -100,10 +101,10 @@ def _normals(rows: np.ndarray, seed: int, offset: int) -> np.ndarray:
 def test_full_size_policy_rollout_sampled(pkg, venv):
     """BASELINE config 2 (65,536 formations x 10 agents) through the fused PPO collection kernel
     (fenv_policy_rollout: policy + Gaussian sample + clip + env step x 10, last value, GAE), a
-    sample of formations checked against the CPU oracles: the policy against
-    oracle/policy_oracle.py (tolerance 2e-5 + 2e-5|ref|, as tests/test_gpu_policy.py), the noise
-    against its Philox restatement, every env transition bit for bit against the C oracle, GAE
-    against SB3's recurrence."""
+    sample of formations checked against the CPU oracles: the policy (mu, value, action,
+    log_prob, last value) against oracle/policy_oracle.py + the Philox noise restatement at the
+    north star's 1e-5 relative (tests/tolerance.py), every env transition bit for bit against the
+    C oracle, GAE against SB3's recurrence."""
     from importlib import import_module
 
     import policy_oracle as po
@@ -141,18 +142,19 @@ def test_full_size_policy_rollout_sampled(pkg, venv):
 
     sd = po.unflatten(pol.flat.detach().cpu(), D)
     mu_ref, v_ref = po.forward(sd, obs.reshape(-1, D))
-    torch.testing.assert_close(mu.reshape(-1, 2), mu_ref, atol=2e-5, rtol=2e-5)
-    torch.testing.assert_close(val.reshape(-1), v_ref, atol=2e-5, rtol=2e-5)
-    std = sd["log_std"].exp()
+    assert_rel_close(mu.reshape(-1, 2), mu_ref, "mu")
+    assert_rel_close(val.reshape(-1), v_ref, "value")
+    std = sd["log_std"].exp().double()
+    mu_ref = mu_ref.reshape(T, S, 2).double()
     for j in range(T):
-        eps = torch.from_numpy(_normals(ag, 11, off0 + j)).float()
-        torch.testing.assert_close(act[j], mu[j] + std * eps, atol=5e-5, rtol=5e-5)
+        eps = torch.from_numpy(_normals(ag, 11, off0 + j))
+        assert_rel_close(act[j], mu_ref[j] + std * eps, f"action step {j}")
     assert torch.equal(clp, act.clamp(-1, 1))
-    torch.testing.assert_close(lp.reshape(-1), po.log_prob(sd, mu.reshape(-1, 2),
-                                                           act.reshape(-1, 2)),
-                               atol=1e-4, rtol=1e-5)
+    assert_rel_close(lp.reshape(-1), po.log_prob({"log_std": sd["log_std"].double()},
+                                                 mu_ref.reshape(-1, 2),
+                                                 act.reshape(-1, 2).double()), "log_prob")
     _, lv_ref = po.forward(sd, last_obs)
-    torch.testing.assert_close(last_val, lv_ref, atol=2e-5, rtol=2e-5)
+    assert_rel_close(last_val, lv_ref, "last value")
 
     ref = COracleEnv(len(fs), N, True, 0)
     ref.set_state(pre[0][ag], pre[1][ag], pre[2][fs], pre[3][fs], pre[4][fs])
@@ -209,9 +211,9 @@ def test_beyond_int32_sizes_sampled_vs_oracle(venv, F, N, goal, T):
     part = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
     seed = 91
     if T == 1:  # reuse the env's own [A, D] / [A] buffers (memory)
-        obs, rew, done = env.rollout_random(1, seed, 0, obs=env.obs_dev, rew=env.rew_dev,
-                                            done=env.done_dev, partial=part)
-        obs, rew, done = obs.view(1, A, D), rew.view(1, A), done.view(1, A)
+        obs, rew, done = env.rollout_random(1, seed, 0, obs=env.obs_dev.view(1, A, D),
+                                            rew=env.rew_dev.view(1, A),
+                                            done=env.done_dev.view(1, A), partial=part)
     else:
         obs, rew, done = env.rollout_random(T, seed, 0, partial=part)
     sums = env.reduce_partials(part).cpu().numpy()

@@ -290,10 +290,130 @@ def test_metrics_and_partials(venv):
     assert sums[1] == ds
     m = env.metrics(rew[-1]).cpu().numpy()
     mr = ref.metrics(rew[-1].cpu().numpy())
+    assert m.shape == (F, 8)
     np.testing.assert_allclose(m, mr, rtol=1e-5, atol=1e-4)
-    s = torch.zeros(4, dtype=torch.float64, device=DEV)
+    s = torch.zeros(8, dtype=torch.float64, device=DEV)
     env.metrics(rew[-1], sums=s)
     np.testing.assert_allclose(s.cpu().numpy(), mr.sum(0), rtol=1e-5)
+
+
+@pytest.mark.parametrize("N,mode", [(5, "mt19937"), (10, "philox"), (1, "mt19937"),
+                                    (64, "philox"), (100, "mt19937")])
+def test_reward_components_every_step_incl_done(venv, N, mode):
+    """fenv_metrics columns 4-7: the means of compute_reward_and_done's logged components
+    (simulate.py:183-208) of the state each step scored -- on a done step the terminal
+    (pre-reset) state -- against the C oracle, whose components are pinned to the reference's
+    own wandb logs (tests/test_oracle_golden.py).  Summed in agent order in double from
+    bit-identical fp32 terms: equal as float32.  Philox mode: the oracle is re-synchronised to
+    the GPU state before each step (its MT19937 resets draw other positions, but the scored
+    pre-reset state is the same)."""
+    F, max_steps = 37, 4
+    env = make_env(venv, F, N, True, 8, max_steps=max_steps, reset_mode=mode)
+    ref = COracleEnv(F, N, True, 8, max_steps=max_steps)
+    env.reset()
+    ref.reset()
+    if mode == "philox":  # the GPU's reset draws come from Philox: start the oracle there
+        ref.set_state(*(v.cpu().numpy() for v in env.get_state()))
+    m0 = env.metrics().cpu().numpy()
+    assert np.array_equal(m0[:, 4:].astype(np.float32), ref.metrics()[:, 4:].astype(np.float32))
+    dones = 0
+    for k in range(1, 15):
+        if mode == "philox":
+            ref.set_state(*(v.cpu().numpy() for v in env.get_state()))
+        a = synth_actions(13, k, F * N, 1.2)
+        _, rw, d, _ = env.step(a)
+        _, rr, rd, _ = ref.step(a)
+        assert np.array_equal(d, rd)
+        dones += int(d.any())
+        m = env.metrics(torch.from_numpy(rw).to(DEV)).cpu().numpy()
+        mr = ref.metrics(rr).astype(np.float32)
+        assert np.array_equal(bits(m[:, 4:]), bits(mr[:, 4:])), f"step {k}"
+        if mode == "mt19937":
+            np.testing.assert_allclose(m[:, :4], mr[:, :4], rtol=1e-5, atol=1e-4)
+    assert dones >= 2  # episodes of max_steps + 2 = 6 steps: done steps 6 and 12
+    # after a reset / set_state the components describe the current state
+    env.reset()
+    ref.reset()
+    if mode == "philox":
+        ref.set_state(*(v.cpu().numpy() for v in env.get_state()))
+    assert np.array_equal(bits(env.metrics().cpu().numpy()[:, 4:]),
+                          bits(ref.metrics()[:, 4:].astype(np.float32)))
+
+
+def test_sb3_vecenv_base_on_device(venv):
+    """With an SB3 stand-in importable, the constructed env IS a VecEnv, initialised by the base
+    class with the reference's arguments (vectorized_env.py:16, 36), and every reference stub
+    keeps its exception type (vectorized_env.py:87-109)."""
+    import importlib
+    import sys
+    import types
+
+    rec = {}
+
+    class VecEnv:
+        def __init__(self, num_envs, observation_space, action_space):
+            rec.update(n=num_envs, obs=observation_space, act=action_space)
+            try:
+                self.get_attr("render_modes")
+            except AttributeError:
+                rec["get_attr_raised"] = True
+
+    saved = {k: sys.modules.get(k) for k in ("stable_baselines3", "stable_baselines3.common",
+                                               "stable_baselines3.common.vec_env")}
+    try:
+        for k in saved:
+            sys.modules[k] = types.ModuleType(k)
+        sys.modules["stable_baselines3.common.vec_env"].VecEnv = VecEnv
+        ve = importlib.reload(venv)
+        env = ve.FormationEnv({"num_formation": 9, "num_agents_per_formation": 5,
+                               "goal_in_obs": True}, device=DEV, seed=3)
+        assert isinstance(env, VecEnv)
+        assert rec["n"] == 45 and tuple(rec["obs"].shape) == (8,) and rec["get_attr_raised"]
+        assert env.num_envs == 45 and env.observation_space is rec["obs"]
+        o = env.reset()
+        obs, rew, done, infos = env.step(np.zeros((45, 2), np.float32))
+        assert o.shape == obs.shape == (45, 8) and len(infos) == 45
+        for m, args, exc in (("close", (), NotImplementedError),
+                             ("get_attr", ("x",), AttributeError),
+                             ("set_attr", ("x", 1), NotImplementedError),
+                             ("env_method", ("x",), NotImplementedError),
+                             ("env_is_wrapped", (object,), NotImplementedError),
+                             ("seed", (1,), NotImplementedError),
+                             ("step_async", (None,), NotImplementedError),
+                             ("step_wait", (), NotImplementedError)):
+            with pytest.raises(exc):
+                getattr(env, m)(*args)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+        importlib.reload(venv)
+
+
+def test_caller_buffers_validated(venv):
+    """Output buffers handed to the kernels as raw pointers are checked first (wrong shape or
+    dtype -> ValueError, nothing launched)."""
+    F, N, T = 20, 5, 3
+    env = make_env(venv, F, N, True, 1, reset_mode="philox")
+    A = F * N
+    acts = torch.zeros((T, A, 2), device=DEV)
+    bad = [dict(obs=torch.empty((T, A, 6), device=DEV)),
+           dict(rew=torch.empty((T, A - 1), device=DEV)),
+           dict(done=torch.empty((T, A), device=DEV)),                      # float32, not bool
+           dict(partial=torch.empty(1, device=DEV))]
+    for kw in bad:
+        with pytest.raises(ValueError):
+            env.rollout(acts, **kw)
+    with pytest.raises(ValueError):
+        env.step_tensor(acts[0], done=torch.empty(A, dtype=torch.uint8, device=DEV).float())
+    with pytest.raises(ValueError):
+        env.rollout_random(T, 1, 0, obs=torch.empty((T + 1, A, 8), device=DEV))
+    with pytest.raises(ValueError):
+        env.metrics(sums=torch.zeros(4, dtype=torch.float64, device=DEV))
+    obs, rew, done = env.rollout(acts)  # the valid call still works
+    assert obs.shape == (T, A, 8) and done.dtype == torch.bool
 
 
 @pytest.mark.parametrize("op", [0, 1, 2, 3])

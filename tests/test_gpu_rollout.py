@@ -3,9 +3,15 @@
 GAE is checked against a numpy restatement of SB3 RolloutBuffer.compute_returns_and_advantage
 (parity unpinned vs SB3 itself, which is not installed); the rollout against step-by-step
 policy + env calls; the training-side torch model against the HIP policy kernel."""
+import os
+import socket
+
 import numpy as np
 import pytest
 import torch
+import torch.multiprocessing as mp
+
+from tolerance import assert_rel_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -81,8 +87,8 @@ def test_torch_model_matches_kernel(mods):
     obs = torch.rand((5000, 8), device=DEV) * 2 - 1
     r = pol.forward(obs, seed=1, offset=0)
     v, lp, ent = mods["ppo"].evaluate_actions(pol, pol.flat, obs, r["action"])
-    torch.testing.assert_close(v, r["value"], atol=2e-5, rtol=2e-5)
-    torch.testing.assert_close(lp, r["log_prob"], atol=1e-4, rtol=1e-5)
+    assert_rel_close(r["value"], v, "value")
+    assert_rel_close(r["log_prob"], lp, "log_prob")
     assert torch.allclose(ent, torch.full_like(ent, 2 * (0.5 + 0.5 * np.log(2 * np.pi))))
 
 
@@ -218,3 +224,106 @@ def test_fused_update_matches_torch(mods, goal):
     torch.testing.assert_close(v1, v0, atol=1e-9, rtol=1e-3)
     for k in s0:
         assert abs(s0[k] - s1[k]) <= 1e-4 * max(1.0, abs(s0[k])), (k, s0[k], s1[k])
+
+
+@pytest.mark.parametrize("mode", ["mt19937", "philox"])
+def test_sharded_rollouts_concatenate_to_unsharded(mods, mode):
+    """Shards of one batch (uneven: 26 + 25 formations) collect, between them, exactly the
+    unsharded rollout: env shards are bit-exact (MT19937 skip-ahead / Philox by global
+    formation) and the policy noise is keyed by global agent index (fenv_policy_rollout,
+    policy_forward row0).  Fused and per-step paths alike, several rollouts with resets."""
+    ve, ro = mods["vectorized_env"], mods["rollout"]
+    F, N, T = 51, 5, 10
+    pol = mods["policy"].MlpPolicy(8, device=DEV, seed=6)
+    with torch.no_grad():
+        pol.flat.add_(torch.randn(pol.flat.shape, generator=torch.Generator().manual_seed(1))
+                      .to(DEV) * 0.05)
+    cfg = lambda f: {"num_formation": f, "num_agents_per_formation": N, "goal_in_obs": True}  # noqa
+    for fused in (True, False):
+        whole = ve.FormationEnv(cfg(F), device=DEV, seed=9, reset_mode=mode, max_steps=12)
+        parts = [ve.FormationEnv(cfg(c), device=DEV, seed=9, reset_mode=mode, max_steps=12,
+                                 first_formation=f0, total_formations=F)
+                 for f0, c in ((0, 26), (26, 25))]
+        bufs = [ro.RolloutBuffer(T, e.num_envs, 8, DEV) for e in [whole] + parts]
+        cols = [ro.RolloutCollector(e, pol, b, seed=21, fused=fused)
+                for e, b in zip([whole] + parts, bufs)]
+        for r in range(3):
+            for c in cols:
+                c.collect()
+            torch.cuda.synchronize()
+            for name in FIELDS:
+                cat = torch.cat([getattr(bufs[1], name), getattr(bufs[2], name)], dim=1)
+                assert torch.equal(getattr(bufs[0], name), cat), (fused, r, name)
+        assert bool(bufs[0].dones.any()) or bool(torch.cat([b.dones for b in bufs]).any())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ppo_rank(rank, world, port, q, F, kw):
+    """One rank of a world-2 PPO run on cuda:0 (gloo: both ranks share the one GPU)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import pkgload
+    pkg = pkgload.load()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".distributed")
+    ve = import_module(pkg.__name__ + ".vectorized_env")
+    ppo_mod = import_module(pkg.__name__ + ".ppo")
+    d.init_from_env(backend="gloo")
+    first, count = d.shard_range(F, rank, world)
+    env = ve.FormationEnv({"num_formation": count, "num_agents_per_formation": 5,
+                           "goal_in_obs": True}, device=DEV, seed=2, first_formation=first,
+                          total_formations=F, **kw["env"])
+    m = ppo_mod.PPO(env, ppo_mod.PPOConfig(**kw["ppo"]), seed=3)
+    m.learn(total_timesteps=kw["timesteps"])
+    st = m.opt.state[m.param]
+    q.put((rank, m.policy.flat.cpu().numpy().tobytes(), st["exp_avg"].cpu().numpy().tobytes(),
+           float(st["step"]), m.num_timesteps, m._gsamples.cpu().numpy().tobytes()))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch_size,n_epochs", [(64, 2), (512, 2)])  # fused kernel / graphs
+def test_two_rank_ppo_equals_single_process(mods, batch_size, n_epochs):
+    """World-2 training (uneven shards 26 + 25 formations, gloo, both ranks on this GPU): one
+    all-gather of the samples per update, the same update on every rank -- both ranks end with
+    bitwise identical parameters and Adam state, equal to a single-process run on the unsharded
+    env (which also equals train() on the concatenated shard buffers), and agree on
+    num_timesteps.  No per-minibatch collective exists to hang on uneven shards."""
+    F = 51
+    kw = {"env": {"reset_mode": "mt19937", "max_steps": 12},
+          "ppo": {"batch_size": batch_size, "n_epochs": n_epochs}, "timesteps": F * 5 * 10 * 3}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_rank, args=(r, 2, port, q, F, kw)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=300), q.get(timeout=300)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # single process, unsharded
+    env = mods["vectorized_env"].FormationEnv({"num_formation": F, "num_agents_per_formation": 5,
+                                               "goal_in_obs": True}, device=DEV, seed=2,
+                                              **kw["env"])
+    m = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(**kw["ppo"]), seed=3)
+    m.learn(total_timesteps=kw["timesteps"])
+    st = m.opt.state[m.param]
+    assert m.num_timesteps == res[0][3] == res[1][3] == kw["timesteps"]
+    assert res[0][0] == res[1][0], "ranks' parameters differ"
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2], "ranks' Adam states differ"
+    assert res[0][4] == res[1][4], "ranks gathered different samples"
+    b = m.buffer
+    D = 8
+    g = np.frombuffer(res[0][4], np.float32).reshape(10, F * 5, D + 5)
+    assert np.array_equal(g[..., :D], b.observations.cpu().numpy())
+    assert np.array_equal(g[..., D + 3], b.advantages.cpu().numpy())
+    assert res[0][0] == m.policy.flat.cpu().numpy().tobytes(), "world-2 != single process"
+    assert res[0][1] == st["exp_avg"].cpu().numpy().tobytes()
