@@ -138,6 +138,19 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
         col.collect()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # the fused collection kernel alone (no GAE launch), HIP events on its stream
+    bufs = dict(obs=buf.observations, mu=buf.mu, action=buf.actions, clipped=buf.clipped,
+                value=buf.values, log_prob=buf.log_probs, reward=buf.rewards,
+                episode_start=buf.episode_starts, done=buf.dones,
+                last_done=col.last_episode_starts, last_obs=col.last_obs,
+                last_value=col._last_values)
+    ka, kb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ka.record()
+    for r in range(rollouts):
+        env.policy_rollout(pol.flat, 10, bufs, seed=0, offset=1000 + 10 * r)
+    kb.record()
+    torch.cuda.synchronize()
+    pr_ms = ka.elapsed_time(kb) / rollouts
     # policy kernel alone, HIP events on its stream
     obs = buf.observations[0]
     out = dict(mu=buf.mu[0], value=buf.values[0], action=buf.actions[0],
@@ -155,6 +168,8 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
     return {"workload": f"config2: {formations} formations x {agents} agents, PPO rollout "
                         f"(n_steps=10): fused MFMA policy forward + env step per step, GAE",
             "value": A * 10 * rollouts / el, "unit": "agent-steps/s",
+            "rollout_kernel_ms": pr_ms,
+            "roofline": policy_rollout_roofline(pr_ms),
             "policy_kernel_ms": pk_ms,
             "policy_fp32_equiv_tflops": flop / (pk_ms * 1e-3) / 1e12,
             "policy_f16_mfma_tflops": f16 / (pk_ms * 1e-3) / 1e12,
@@ -162,6 +177,36 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
             "f16_mfma_frac": f16 / (pk_ms * 1e-3) / 1e12 / 2516.6,
             "arithmetic": "split-f16 MFMA (hi*hi + hi*lo + lo*hi, fp32 accumulate), fp32 tanh/heads",
             "bound": "VALU issue (256 exp+rcp tanh per agent-step), see DESIGN.md"}
+
+
+SIMDS, SCLK_HZ = 1024, 2.4e9  # MI355X: 256 CUs x 4 SIMDs, 2.4 GHz peak engine clock
+
+
+def policy_rollout_roofline(kernel_ms: float):
+    """Roofline of the fused policy rollout (k_policy_rollout): it is bound by VALU issue, not by
+    HBM (~78 B per agent-step) or the MFMA pipe.  achieved = the kernel's VALU-active SIMD-cycles
+    per launch (SQ_ACTIVE_INST_VALU x 4, PMC, profiles/r2_policy_pmc_sq.json) / the launch time
+    measured live in this run; peak = every SIMD's VALU busy every cycle (1024 x 2.4 GHz).
+    mfma_busy_frac the same way from SQ_VALU_MFMA_BUSY_CYCLES."""
+    p = os.path.join(ROOT, "profiles", "r2_policy_pmc_sq.json")
+    if not os.path.exists(p):
+        return None
+    ks = json.load(open(p)).get("kernels", {})
+    k = next((v for n, v in ks.items() if "k_policy_rollout" in n), None)
+    if not k or "SQ_ACTIVE_INST_VALU" not in k:
+        return None
+    peak = SIMDS * SCLK_HZ
+    valu = 4.0 * k["SQ_ACTIVE_INST_VALU"] / (kernel_ms * 1e-3)
+    out = {"bound": "valu-issue", "achieved": valu, "peak": peak,
+           "unit": "VALU-active SIMD-cycles/s", "frac": valu / peak,
+           "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
+           "kernel": "k_policy_rollout (fenv_policy_rollout)", "kernel_ms": kernel_ms,
+           "pmc_source": "profiles/r2_policy_pmc_sq.json"}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in k:
+        out["mfma_busy_frac"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (kernel_ms * 1e-3) / peak
+    if "SQ_WAVE_CYCLES" in k:
+        out["avg_waves_per_simd"] = 4.0 * k["SQ_WAVE_CYCLES"] / (kernel_ms * 1e-3) / peak
+    return out
 
 
 def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: int = 50,
@@ -398,16 +443,30 @@ def main():
                 released[s].record(side)
             nstat[0] += 1
 
-    # 1) pre-warm by device time (clocks, first touch of the 2 GB rollout buffer, and the first
-    # launch of every kernel the timed region uses -- a kernel's first launch in a process costs
-    # milliseconds of host time, e.g. the stats reduction's), then 2) exactly --warmup steps,
-    # 3) exactly --steps timed steps.
+    def region(plan, stat_every, evs=None):
+        """The timed region's work: the launches of `plan`, stats every `stat_every` launches,
+        then the wait for the stats (side stream / all-reduce)."""
+        if evs is not None:
+            evs[0].record(main_s)
+        for k, L in enumerate(plan):
+            launch(L, stat=not args.no_stats and (k + 1) % stat_every == 0)
+            if evs is not None:
+                evs[k + 1].record(main_s)
+        if not args.no_stats:
+            main_s.wait_stream(side)
+            return stats.result()
+        return None
+
+    # 1) pre-warm by device time: clocks, first touch of the 2 GB rollout buffer, and the first
+    # use of every kernel, stream and event the timed region uses (a kernel's first launch or a
+    # stream's first use in a process costs milliseconds of host time -- e.g. the stats
+    # reduction kernel, the stats reducer's stream); 2) exactly --warmup steps; 3) exactly
+    # --steps timed steps.
     pw_launches, pw_ms = 0, 0.0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     while pw_ms < args.prewarm_ms and pw_launches < 100000:
         e0.record(main_s)
-        for j in range(5):
-            launch(T, stat=not args.no_stats and j == 4)
+        region([T] * 5, 5)
         e1.record(main_s)
         e1.synchronize()
         pw_launches += 5
@@ -423,14 +482,8 @@ def main():
     stat_every = max(1, min(args.stats_every, len(plan)))
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
     t0 = time.perf_counter()
-    evs[0].record(main_s)
-    for k, L in enumerate(plan):
-        launch(L, stat=not args.no_stats and (k + 1) % stat_every == 0)
-        evs[k + 1].record(main_s)
+    tot = region(plan, stat_every, evs)
     t_issued = time.perf_counter() - t0
-    if not args.no_stats:
-        main_s.wait_stream(side)
-        tot = stats.result()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

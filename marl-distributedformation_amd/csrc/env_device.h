@@ -20,6 +20,28 @@ __device__ __forceinline__ float norm2(float x, float y) {
     return __builtin_sqrtf(__builtin_fmaf(y, y, xx));
 }
 
+// x / Y (Y = 400 or 600), correctly rounded.  FENV_DIV_CONST=1: q0 = x*RN(1/Y) plus one fma
+// residual correction (3 dependent ops instead of the ~10 of the IEEE division sequence), which
+// equals IEEE x/Y for every finite |x| >= 2^-100 (tools/div_const_check.c, exhaustive); the
+// IEEE division is kept behind a branch for the rest (tiny, inf, NaN).  Default off (A/B'd per
+// config: profiles/ab/).
+#ifndef FENV_DIV_CONST
+#define FENV_DIV_CONST 0
+#endif
+template <int Y>
+__device__ __forceinline__ float div_const(float x) {
+#if FENV_DIV_CONST
+    constexpr float y = (float)Y;
+    constexpr float c = 1.0f / (float)Y;
+    if (__builtin_expect(__builtin_fabsf(x) >= 0x1p-100f && __builtin_fabsf(x) <= 0x1p+127f, 1)) {
+        const float q0 = x * c;
+        const float r = __builtin_fmaf(-q0, y, x);
+        return __builtin_fmaf(r, c, q0);
+    }
+#endif
+    return x / (float)Y;
+}
+
 // torch.clip(v, 0, hi) incl. NaN propagation (simulate.py:89-90)
 __device__ __forceinline__ float clip0(float v, float hi) {
     return v < 0.0f ? 0.0f : (v > hi ? hi : v);
@@ -189,8 +211,8 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
 // compute_obs (simulate.py:150-174) of this lane's agent into o[0..D).
 template <int D, class X>
 __device__ __forceinline__ void env_obs(const X &x, const Agent &s, float (&o)[8]) {
-    const float nx = s.px / kW;  // :156, normalise first
-    const float ny = s.py / kH;
+    const float nx = div_const<400>(s.px);  // :156, normalise first
+    const float ny = div_const<600>(s.py);
     float npx, nnx, npy, nny;
     x.d_pn(nx, ny, npx, nnx, npy, nny);
     o[0] = nx;
@@ -200,8 +222,8 @@ __device__ __forceinline__ void env_obs(const X &x, const Agent &s, float (&o)[8
     o[4] = nnx - nx;  // :167
     o[5] = nny - ny;
     if (D == 8) {
-        o[6] = (s.gx - s.px) / kW;  // :172, subtract first, then divide
-        o[7] = (s.gy - s.py) / kH;
+        o[6] = div_const<400>(s.gx - s.px);  // :172, subtract first, then divide
+        o[7] = div_const<600>(s.gy - s.py);
     }
 }
 

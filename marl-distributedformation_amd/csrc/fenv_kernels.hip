@@ -100,7 +100,7 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
     }
 }
 
-template <int D, int MODE, bool RA, bool RS, class X>
+template <int D, int MODE, bool RA, bool RS, int PF, class X>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
@@ -121,11 +121,10 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
     }
     bool any_reset = false;
     // Rolling action prefetch: a ring of kPF registers keeps the loads of the next kPF steps in
-    // flight while a step computes (kPF = 1: load step k+1 during step k).
-#ifndef FENV_ACT_PREFETCH
-#define FENV_ACT_PREFETCH 1
-#endif
-    constexpr int kPF = (RA || RS) ? 1 : FENV_ACT_PREFETCH;  // staged rows: one-step prefetch
+    // flight while a step computes (kPF = 1: load step k+1 during step k).  The step loop is
+    // unrolled by kPF, which also lets the scheduler overlap one step's observation / reward
+    // tail with the next step's head: what a latency-bound small grid wants (see use_pf).
+    constexpr int kPF = (RA || RS) ? 1 : PF;  // staged rows / in-kernel actions: one step
     float2 ring[kPF];
     const int64_t ga = c.f0 * c.N + a;  // global agent index (shard-invariant actions)
     uint4 words = make_uint4(0u, 0u, 0u, 0u);
@@ -202,7 +201,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
     }
 }
 
-template <int D, int MODE, bool RA>
+template <int D, int MODE, bool RA, int PF>
 __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, DevPending p,
                                                       int32_t T, const float2 *__restrict__ act,
                                                       ActGen gen,
@@ -229,8 +228,9 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
     const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
     float rsum = 0.f, dsum = 0.f;
     if (M > 0)
-        rollout_body<D, MODE, RA, false>(c, st, p, x, active, f, a, i, stage[w], lane, M,
-                                         f_first * N, T, act, gen, obs, rew, done, rsum, dsum);
+        rollout_body<D, MODE, RA, false, PF>(c, st, p, x, active, f, a, i, stage[w], lane, M,
+                                             f_first * N, T, act, gen, obs, rew, done, rsum,
+                                             dsum);
     if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -283,8 +283,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     rsg.g0 = blk * kRS * Mw;
     rsg.nwg = (int)((A - rsg.g0) < (int64_t)kRS * Mw ? (A - rsg.g0) : (int64_t)kRS * Mw);
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA, true>(c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N,
-                                    T, act, gen, obs, rew, done, rsum, dsum, rsg);
+    rollout_body<D, MODE, RA, true, 1>(c, st, p, x, active, f, a, i, stage[w], lane, M,
+                                       f_first * N, T, act, gen, obs, rew, done, rsum, dsum, rsg);
     if (partial) {  // one {sum reward, sum done} record per 4 waves -- the same records, in the
                     // same summation order, as k_rollout_wave's 4-wave workgroups
         rsum = wave_sum(rsum);
@@ -326,8 +326,8 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     const int w = i >> 6;
     const int M = N - 64 * w < 64 ? (N - 64 * w > 0 ? N - 64 * w : 0) : 64;
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA, false>(c, st, p, x, active, f, a, i, stage[w], i & 63, M,
-                                     f * N + 64 * w, T, act, gen, obs, rew, done, rsum, dsum);
+    rollout_body<D, MODE, RA, false, 1>(c, st, p, x, active, f, a, i, stage[w], i & 63, M,
+                                        f * N + 64 * w, T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {
         rsum = wave_sum(rsum);
         dsum = wave_sum(dsum);
@@ -619,6 +619,19 @@ static inline bool use_rs(const Consts &c, int32_t T) {
     return (c.fpw * c.N) % 32 != 0 && waves >= FENV_RS_MIN_WAVES;
 }
 
+// Small latency-bound grids (fewer waves than FENV_RS_MIN_WAVES: the per-step dependency chain
+// of one wave, not HBM, sets the time) take a 4-deep action prefetch / 4x unrolled step loop:
+// same-box A/B at BASELINE config 1 (4,096 x 5) 10.04-10.08 vs 10.47 us per 10-step launch,
+// while it costs 5-7 % at config 4 (16,384 x 64, 16,384 waves), which keeps depth 1
+// (profiles/ab/r2_env_cfg_ab.txt).
+#ifndef FENV_SMALL_PF
+#define FENV_SMALL_PF 4
+#endif
+static inline bool use_pf(const Consts &c, int32_t T) {
+    const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
+    return FENV_SMALL_PF > 1 && T >= FENV_SMALL_PF && waves < FENV_RS_MIN_WAVES;
+}
+
 int64_t rollout_group_count(const Consts &c) {
 #if FENV_RW
     if (wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
@@ -645,7 +658,7 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
                                dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p,
                                T, a2, *gen, obs, rew, done, p2, accum);
         else if (wave_path(c.N))
-            hipLaunchKernelGGL((k_rollout_wave<D, MODE, true>), dim3((unsigned)group_count(c)),
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, true, 1>), dim3((unsigned)group_count(c)),
                                dim3(256), 0, st, c, s, p, T, a2, *gen, obs, rew, done, p2, accum);
         else
             hipLaunchKernelGGL((k_rollout_block<D, MODE, true>), dim3((unsigned)c.F),
@@ -668,8 +681,12 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
                            a2, g0, obs, rew, done, p2, accum);
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
-        hipLaunchKernelGGL((k_rollout_wave<D, MODE, false>), dim3(blocks), dim3(256), 0, st, c, s,
-                           p, T, a2, g0, obs, rew, done, p2, accum);
+        if (use_pf(c, T))
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, FENV_SMALL_PF>), dim3(blocks),
+                               dim3(256), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
+        else
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, 1>), dim3(blocks), dim3(256), 0, st,
+                               c, s, p, T, a2, g0, obs, rew, done, p2, accum);
     } else {
         hipLaunchKernelGGL((k_rollout_block<D, MODE, false>), dim3((unsigned)c.F),
                            dim3(block_threads(c.N)), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2,
@@ -683,7 +700,8 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
     if (wave_path(c.N)) return "k_rollout_wg";
 #endif
     if (use_rs(c, T)) return "k_rollout_wave_rs";
-    return wave_path(c.N) ? "k_rollout_wave" : "k_rollout_block";
+    if (wave_path(c.N)) return use_pf(c, T) ? "k_rollout_wave (prefetch 4)" : "k_rollout_wave";
+    return "k_rollout_block";
 }
 
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,

@@ -93,8 +93,10 @@ constexpr int oB2 = oB1 + 2 * kHid;        // [net][64]  (b2 + rowsum W2) * kTan
 constexpr int oHA0 = oB2 + 2 * kHid;       // -2 * action_net.weight[0][64]
 constexpr int oHA1 = oHA0 + kHid;          // -2 * action_net.weight[1][64]
 constexpr int oHV = oHA1 + kHid;           // -2 * value_net.weight[0][64]
-constexpr int oSc = oHV + kHid;            // ba0 ba1 bv (each + rowsum) log_std0 log_std1 (+3)
-constexpr int kPolicyLds = oSc + 8;        // 10,696 floats = 42.8 KB
+constexpr int oSc = oHV + kHid;            // ba0 ba1 bv (each + rowsum), log_std[2], then per
+                                           // component h: std[2] at +5, 0.5/var[2] at +7,
+                                           // log(std)[2] at +9 (hoisted out of the step loop)
+constexpr int kPolicyLds = oSc + 12;       // 10,700 floats = 42.8 KB
 
 // x = hi + lo: hi = x truncated to 11 significant bits (exact in f16 for 2^-14 <= |x| < 65504),
 // lo = f16(x - hi) (x - hi is exact).  Two values per v_cvt_pkrtz_f16_f32.
@@ -188,6 +190,12 @@ __device__ __forceinline__ void stage_policy_weights(float *lds, const float *__
             v = params[L.logstd + tid - 3];
         }
         lds[oSc + tid] = v;
+    }
+    if (tid < 2) {  // the Gaussian's per-component constants (torch Normal, scale = exp(log_std))
+        const float sd = expf(params[L.logstd + tid]);
+        lds[oSc + 5 + tid] = sd;
+        lds[oSc + 7 + tid] = 0.5f / (sd * sd);
+        lds[oSc + 9 + tid] = logf(sd);
     }
 }
 
@@ -354,7 +362,7 @@ __device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo
         o.mu = o.act = o.clip = o.logp = 0.0f;
         return o;
     }
-    const float std_h = expf(lds[oSc + 3 + h]);
+    const float std_h = lds[oSc + 5 + h];
     o.mu = pa + lds[oSc + h];
     float a = o.mu;
     if (!deterministic) {
@@ -369,9 +377,9 @@ __device__ __forceinline__ PolicyLane policy_tile(const float *lds, const h8 &bo
     o.act = a;
     o.clip = a < -1.0f ? -1.0f : (a > 1.0f ? 1.0f : a);
     // torch Normal.log_prob: -(a-mu)^2 / (2 var) - log(scale) - log(sqrt(2 pi)), scale = exp(ls)
-    const float inv_2var = 0.5f / (std_h * std_h);
+    const float inv_2var = lds[oSc + 7 + h];
     const float d = a - o.mu;
-    const float lp_h = -(d * d) * inv_2var - logf(std_h) - 0.918938533204672742f;
+    const float lp_h = -(d * d) * inv_2var - lds[oSc + 9 + h] - 0.918938533204672742f;
     o.logp = join_halves(lp_h, h);
     return o;
 }

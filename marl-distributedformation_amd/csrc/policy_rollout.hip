@@ -61,23 +61,14 @@ __device__ __forceinline__ void tile_operands(const float *stage, int j, int h, 
     }
 }
 
+// One wave-unit: the fpw whole formations starting at formation f_first, all T steps (the body
+// of the persistent loop below).
 template <int D, int MODE>
-__global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_rollout(Consts c, DevState st,
-                                                                  DevPending p, PRArgs g) {
-    // Dynamic LDS (kPRLdsBytes, set at launch): with a static 55 KB declaration the compiler
-    // budgets registers for 2 waves/SIMD and schedules into 220+ VGPRs; sized at launch it keeps
-    // the 4 waves/SIMD that the LDS actually allows (2 workgroups per CU).
-    extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
-    float *wimg = lds_dyn;
-    float(*stage_all)[512] = reinterpret_cast<float(*)[512]>(lds_dyn + kPolicyLds);
-    stage_policy_weights(wimg, g.params, D, threadIdx.x, blockDim.x);
-    __syncthreads();  // the only workgroup barrier: waves are independent from here on
-
+__device__ __forceinline__ void policy_rollout_unit(const Consts &c, const DevState &st,
+                                                    const DevPending &p, const PRArgs &g,
+                                                    const float *wimg, float *stage,
+                                                    int64_t f_first) {
     const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR
-    const int64_t wave = (int64_t)blockIdx.x * kPRWaves + w;
-    const int64_t f_first = wave * c.fpw;
-    if (f_first >= c.F) return;
     const int N = c.N;
     const int fi = lane / N;
     const int i = lane - fi * N;
@@ -89,7 +80,6 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
     const int M = (int)((f_left < c.fpw ? f_left : c.fpw) * N);
     const int64_t a_first = f_first * N;
     const int64_t A = c.F * (int64_t)N;
-    float *stage = stage_all[w];
     const fenv_rollout_bufs &b = g.b;
     const bool det = g.deterministic != 0;
 
@@ -196,6 +186,7 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         }
         __builtin_amdgcn_wave_barrier();
         lv = stage[384 + lane];
+        __builtin_amdgcn_wave_barrier();  // the slice is reused by the wave's next unit
     }
     if (active) {
         b.last_done[a] = (uint8_t)start;
@@ -213,13 +204,57 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
     }
 }
 
+// Persistent workgroups (grid = the resident workgroup count, or fewer): the weight image is
+// staged once per workgroup, then every wave walks wave-units wave, wave + G, ... (G = the
+// grid's wave count) with no further barrier, so a finished wave's slot never waits for its
+// workgroup siblings and no workgroup re-stages the weights.
+template <int D, int MODE>
+__global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_rollout(Consts c, DevState st,
+                                                                  DevPending p, PRArgs g) {
+    // Dynamic LDS (kPRLdsBytes, set at launch): with a static declaration of this size the
+    // compiler budgets registers for fewer waves/SIMD than the LDS allows.
+    extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+    float *wimg = lds_dyn;
+    float(*stage_all)[512] = reinterpret_cast<float(*)[512]>(lds_dyn + kPolicyLds);
+    stage_policy_weights(wimg, g.params, D, threadIdx.x, blockDim.x);
+    __syncthreads();  // the only workgroup barrier: waves are independent from here on
+
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR
+    const int64_t stride = (int64_t)gridDim.x * kPRWaves;
+#pragma unroll 1
+    for (int64_t wave = (int64_t)blockIdx.x * kPRWaves + w; wave * c.fpw < c.F; wave += stride)
+        policy_rollout_unit<D, MODE>(c, st, p, g, wimg, stage_all[w], wave * c.fpw);
+}
+
+#ifndef FENV_PR_PERSISTENT
+#define FENV_PR_PERSISTENT 1  // 0: one wave-unit per wave (a workgroup per 4 units), A/B
+#endif
+
 template <int D, int MODE>
 static hipError_t policy_rollout_dm(const Consts &c, const DevState &s, const DevPending &p,
                                     const PRArgs &g, hipStream_t st) {
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
-    const unsigned blocks = (unsigned)((waves + kPRWaves - 1) / kPRWaves);
-    hipLaunchKernelGGL((k_policy_rollout<D, MODE>), dim3(blocks), dim3(64 * kPRWaves), kPRLdsBytes,
-                       st, c, s, p, g);
+    int64_t blocks = (waves + kPRWaves - 1) / kPRWaves;
+    if (FENV_PR_PERSISTENT) {
+        static int resident = 0;  // per template instance (D, MODE)
+        if (resident == 0) {
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_policy_rollout<D, MODE>,
+                                                             64 * kPRWaves, kPRLdsBytes) !=
+                    hipSuccess ||
+                per_cu < 1)
+                per_cu = 1;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                    hipSuccess ||
+                cus < 1)
+                cus = 256;
+            resident = per_cu * cus;
+        }
+        if (blocks > resident) blocks = resident;
+    }
+    hipLaunchKernelGGL((k_policy_rollout<D, MODE>), dim3((unsigned)blocks), dim3(64 * kPRWaves),
+                       kPRLdsBytes, st, c, s, p, g);
     return hipGetLastError();
 }
 

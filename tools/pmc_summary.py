@@ -32,7 +32,7 @@ f_kb = sum(fetch) / len(fetch)
 w_kb = sum(write) / len(write)
 res = {
     "workload": "config3: 1048576 formations x 5 agents (1048576 per GPU x 1), fused 10-step rollouts, philox resets",
-    "kernel": "k_rollout_wave",
+    "kernel": "k_rollout_wave_rs",
     "dispatches": [len(fetch), len(write)],
     "FETCH_SIZE_kib_per_launch": f_kb,
     "WRITE_SIZE_kib_per_launch": w_kb,
