@@ -462,15 +462,28 @@ def main():
     # stream's first use in a process costs milliseconds of host time -- e.g. the stats
     # reduction kernel, the stats reducer's stream); 2) exactly --warmup steps; 3) exactly
     # --steps timed steps.
+    # The number of pre-warm regions is agreed over the ranks (each region holds a stats
+    # all-reduce, so every rank must run the same count): one calibration region, then the
+    # max over ranks of the regions still needed.
     pw_launches, pw_ms = 0, 0.0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    while pw_ms < args.prewarm_ms and pw_launches < 100000:
+
+    def prewarm_region():
         e0.record(main_s)
         region([T] * 5, 5)
         e1.record(main_s)
         e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    pw_ms += prewarm_region()      # first use of everything (slow)
+    last = prewarm_region()        # calibration: one warm region
+    pw_ms += last
+    pw_launches += 10
+    more = int(pdist.max_over_ranks(min(20000, max(0.0, -(-(args.prewarm_ms - pw_ms) //
+                                                        max(last, 1e-3)))), dev))
+    for _ in range(more):
+        pw_ms += prewarm_region()
         pw_launches += 5
-        pw_ms += e0.elapsed_time(e1)
     for L in launch_plan(args.warmup, T):
         launch(L)
     torch.cuda.synchronize()
