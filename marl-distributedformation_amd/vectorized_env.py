@@ -147,6 +147,7 @@ class FormationEnv(_BASE):
                                      _lib.RESET_MODES[mode], self.first_formation,
                                      self.total_formations), "fenv_create")
         self._h = h
+        self._npartial = int(L.fenv_partial_count(h))
         A, D, F = self.num_envs, self.obs_dim, self.num_formation
         dev = self.device
         # device buffers (vectorized_env.py:46-48 obs_buf / reward_buf / done_buf)
@@ -297,21 +298,24 @@ class FormationEnv(_BASE):
                    "fenv_observe")
         return self.obs_dev
 
+    def _on_device(self, t) -> bool:
+        return isinstance(t, torch.Tensor) and t.is_cuda and t.get_device() == self.device.index
+
     def _check_out(self, name: str, t, shape: tuple, dtype) -> None:
         """Caller-supplied output buffers go to the kernels as raw pointers: check them first."""
         if t is None:
             return
-        if not isinstance(t, torch.Tensor) or t.device != self.device:
+        if not self._on_device(t):
             raise ValueError(f"{name} must be a tensor on {self.device}")
-        if tuple(t.shape) != tuple(shape) or t.dtype != dtype or not t.is_contiguous():
+        if t.shape != shape or t.dtype != dtype or not t.is_contiguous():
             raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)}, "
                              f"got {t.dtype} {tuple(t.shape)}")
 
     def _check_partial(self, partial) -> None:
         if partial is None:
             return
-        n = self.partial_count()
-        if (not isinstance(partial, torch.Tensor) or partial.device != self.device
+        n = self._npartial
+        if (not self._on_device(partial)
                 or partial.dtype != torch.float32 or not partial.is_contiguous()
                 or partial.numel() < 2 * n):
             raise ValueError(f"partial must be a contiguous float32 tensor on {self.device} with "
@@ -319,9 +323,9 @@ class FormationEnv(_BASE):
 
     def _check_act(self, act: torch.Tensor, lead: tuple) -> torch.Tensor:
         shape = lead + (self.num_envs, 2)
-        if tuple(act.shape) != shape:
+        if act.shape != shape:
             raise AssertionError(f"actions shape {tuple(act.shape)} != {shape}")
-        if act.dtype != torch.float32 or act.device != self.device:
+        if act.dtype != torch.float32 or not self._on_device(act):
             raise TypeError(f"actions must be float32 on {self.device}")
         return act.contiguous()
 
