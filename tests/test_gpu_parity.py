@@ -558,3 +558,35 @@ def test_empty_launches_are_no_ops(venv, mode):
         env.rollout_random(-1, 1, 0)
     with pytest.raises(Exception):
         make_env(venv, 0, N)
+
+
+@pytest.mark.parametrize("F,N,T", [(4096, 5, 10), (65536, 10, 10), (300, 64, 3), (2000, 5, 1)])
+def test_null_outputs_take_general_kernels_same_results(venv, flib, F, N, T):
+    """fenv_rollout with obs or rew/done passed as NULL through the C ABI skips those stores
+    only: the state it leaves and the rows it does write equal the all-outputs launch's, at the
+    staged (65,536 x 10), prefetch-ring (4,096 x 5), one-formation-per-wave (N = 64) and single-step
+    shapes -- including the staged kernel's last workgroup, whose trailing waves hold no agents
+    and must touch nothing."""
+    import ctypes
+    L = flib.lib()
+    envs = [make_env(venv, F, N, True, 5, reset_mode="philox") for _ in range(3)]
+    A = F * N
+    g = torch.Generator(device=DEV).manual_seed(F + T)
+    acts = torch.rand((T, A, 2), device=DEV, generator=g) * 2.4 - 1.2
+    P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    outs = []
+    for e, (wo, wr) in zip(envs, ((True, True), (False, True), (True, False))):
+        e.reset_tensor()
+        obs = torch.full((T, A, 8), -7.0, device=DEV) if wo else None
+        rew = torch.full((T, A), -7.0, device=DEV) if wr else None
+        done = torch.zeros((T, A), dtype=torch.bool, device=DEV) if wr else None
+        flib.check(L.fenv_rollout(e._h, T, P(acts), P(obs), P(rew), P(done), None,
+                                  flib.current_stream(DEV)))
+        outs.append((obs, rew, done, e.get_state()))
+    torch.cuda.synchronize()
+    full, no_obs, no_rew = outs
+    assert torch.equal(full[1], no_obs[1]) and torch.equal(full[2], no_obs[2])
+    assert torch.equal(full[0], no_rew[0])
+    for sa, sb, sc in zip(full[3], no_obs[3], no_rew[3]):
+        assert torch.equal(sa, sb) and torch.equal(sa, sc)
+    assert not (full[0] == -7.0).any() and not (full[1] == -7.0).any()
