@@ -334,6 +334,36 @@ def load_pmc_traffic(workload: str):
     return None, None
 
 
+def hbm_ceiling(acts, obs, rew, done, A: int, T: int, D: int, stream, reps: int = 20):
+    """Same-box HBM ceiling of the rollout's byte mix (tools/calib/hbm_ceiling.hip): the exact
+    streams of one launch (45 B per agent-step at D = 8) with no arithmetic, every access a whole
+    128-B-aligned float4 run, into this run's own rollout buffers, timed with HIP events on the
+    launch stream.  Measured after the timed region, never inside it.  None when the library is
+    not built or the shape does not apply (D != 8)."""
+    import ctypes
+    p = os.path.join(ROOT, "tools", "calib", "libhbm_ceiling.so")
+    if D != 8 or not os.path.exists(p):
+        return None
+    lib = ctypes.CDLL(p)
+    lib.hbm_ceiling_chunk.restype = ctypes.c_int
+    lib.hbm_ceiling_mix_ms.restype = ctypes.c_double
+    lib.hbm_ceiling_mix_ms.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int32,
+                                                               ctypes.c_int32, ctypes.c_void_p]
+    ch = lib.hbm_ceiling_chunk()
+    Ac = A - A % ch
+    if Ac <= 0:
+        return None
+    ms = lib.hbm_ceiling_mix_ms(acts.data_ptr(), obs.data_ptr(), rew.data_ptr(), done.data_ptr(),
+                                Ac, T, reps, ctypes.c_void_p(stream.cuda_stream))
+    if ms <= 0:
+        return None
+    byts = 45.0 * Ac * T
+    return {"achieved": byts / (ms * 1e-3) / 1e9, "unit": "GB/s", "ms_per_launch": ms,
+            "agents": Ac, "steps": T,
+            "kernel": "k_mix (tools/calib/hbm_ceiling.hip): the launch's action read and obs / "
+                      "reward / done writes, no arithmetic, whole aligned float4 runs"}
+
+
 def launch_plan(steps: int, T: int) -> list[int]:
     """Launch lengths covering exactly `steps` env steps in fused chunks of <= T steps."""
     full, rem = divmod(int(steps), int(T))
@@ -514,6 +544,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     per_launch = [evs[k].elapsed_time(evs[k + 1]) for k in range(len(plan))]
+    ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
     kern_total_ms = sum(per_launch)
     full = [ms for ms, L in zip(per_launch, plan) if L == T] or per_launch
     kern_avg_ms = sum(full) / len(full)
@@ -564,6 +595,12 @@ def main():
                          "launch_ms_min": min(per_launch), "launch_ms_max": max(per_launch),
                          "timing": "HIP events on the launch stream at every launch boundary"},
         }
+        if ceiling is not None:
+            ceiling["frac_of_spec"] = ceiling["achieved"] / HBM_PEAK_GBS
+            ceiling["kernel_frac_of_ceiling"] = (bytes_launch / (kern_avg_ms * 1e-3) / 1e9
+                                                 / ceiling["achieved"])
+            ceiling["rank"] = 0
+            out["roofline"]["same_box_ceiling"] = ceiling
         if not args.no_stats:
             t = tot.cpu().tolist()
             out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * plan[-1]),
