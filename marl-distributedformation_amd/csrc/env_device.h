@@ -161,7 +161,8 @@ struct Agent {
 
 // FormationSimulator.step (simulate.py:70-118) for this lane's agent.  Returns the reward
 // (pre-reset state) and done; leaves the post-(auto-)reset state in `s`.
-template <int MODE, class X>
+// TERM = false: leave the terminal-state record to another wave (the split kernel's kRoleState).
+template <int MODE, class X, bool TERM = true>
 __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, const X &x,
                                          int64_t f, int64_t a, int i, float2 act, Agent &s,
                                          float &rw, bool &dn, bool &did_reset) {
@@ -197,9 +198,11 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
         // (simulate.py:183-208) describe it, not the freshly drawn one
         // (indices laundered inside the branch: otherwise the compiler hoists these rarely used
         // addresses out of the step loop into 4 loop-invariant VGPRs)
-        int64_t ta = a;
-        asm volatile("" : "+v"(ta));
-        p.term[ta] = make_float4(s.px, s.py, s.gx, s.gy);
+        if (TERM) {
+            int64_t ta = a;
+            asm volatile("" : "+v"(ta));
+            p.term[ta] = make_float4(s.px, s.py, s.gx, s.gy);
+        }
         const uint32_t ep_new = s.ep + 1;
         draw_reset<MODE>(c, p, f, a, i, ep_new, s.px, s.py, s.gx, s.gy);
         s.t = 0;

@@ -100,7 +100,13 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
     }
 }
 
-template <int D, int MODE, bool RA, bool RS, int PF, class X>
+// Roles of a wave in rollout_body.  kRoleAll: the whole step.  The split kernel (small grids,
+// k_rollout_wave_split) gives one formation group two waves that both carry the state (the
+// kinematics, done and auto-reset are recomputed bit-identically by each): kRoleState writes
+// reward / done / the stats sums / the terminal and final state, kRoleObs only the observations.
+constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2;
+
+template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
@@ -119,6 +125,10 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         s.t = st.t[f];
         s.ep = st.ep[f];
     }
+    // split kernel: every wave of the workgroup has read the state before a kRoleState wave
+    // may write it back (the partner kRoleObs wave of the same formations sits in the same
+    // workgroup)
+    if (ROLE != kRoleAll) __syncthreads();
     bool any_reset = false;
     // Rolling action prefetch: a ring of kPF registers keeps the loads of the next kPF steps in
     // flight while a step computes (kPF = 1: load step k+1 during step k).  The step loop is
@@ -142,19 +152,21 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
                                gen.k0, gen.k1);
             ac = (gs & 1) ? make_float2(act_u24(words.z), act_u24(words.w))
                           : make_float2(act_u24(words.x), act_u24(words.y));
-            if (gen.out && active) reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
+            if (ROLE != kRoleObs && gen.out && active)
+                reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
         } else if (active && k + kPF < T) {
             ring[j] = act[(int64_t)(k + kPF) * A + a];
         }
         float rw;
         bool dn, rs;
-        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        env_step<MODE, X, ROLE != kRoleObs>(c, p, x, f, a, i, ac, s, rw, dn, rs);
         any_reset |= rs;
         const int64_t row = (int64_t)k * A + a;
         float o[8];
         env_obs<D>(x, s, o);
-        if (obs) store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-        if (active) {
+        if (ROLE != kRoleState && obs)
+            store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
+        if (ROLE != kRoleObs && active) {
             if (RS) {
                 const int kb = k % kRSTB;
                 rsg.rbuf[kb * kRSA + rsg.li] = rw;
@@ -187,7 +199,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
             }
         }
     }
-    if (active) {
+    if (ROLE != kRoleObs && active) {
         st.px[a] = s.px;
         st.py[a] = s.py;
         if (i == 0) {
@@ -240,6 +252,62 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
             float2 v = red[0];
             for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
                 v = make_float2(v.x + red[k].x, v.y + red[k].y);
+            if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
+            partial[blockIdx.x] = v;
+        }
+    }
+}
+
+// Small latency-bound grids (use_split): a 4-wave group of formation-waves (k_rollout_wave's
+// workgroup) is run by 8 waves.  Waves 0-3 take kRoleState, waves 4-7 kRoleObs for the same
+// formations, so each wave issues about half of a step's instructions and a SIMD holds two
+// waves whose latencies hide each other.  The stats record is the 4 kRoleState waves' sums in
+// k_rollout_wave's order: the same records.
+template <int D, int MODE, bool RA, int PF>
+__global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState st, DevPending p,
+                                                            int32_t T,
+                                                            const float2 *__restrict__ act,
+                                                            ActGen gen, float *__restrict__ obs,
+                                                            float *__restrict__ rew,
+                                                            uint8_t *__restrict__ done,
+                                                            float2 *__restrict__ partial,
+                                                            bool accum) {
+    __shared__ __attribute__((aligned(16))) float stage[4][64 * 8];
+    __shared__ float2 red[4];
+    const int lane = threadIdx.x & 63;
+    const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = w8 & 3;  // formation-wave of the group
+    const int64_t wave = (int64_t)blockIdx.x * 4 + w;
+    const int N = c.N;
+    const int fi = lane / N;
+    const int i = lane - fi * N;
+    const int64_t f = wave * c.fpw + fi;
+    const bool active = fi < c.fpw && f < c.F;
+    const int64_t a = f * N + i;
+    WaveX x{i == 0 ? lane + N - 1 : lane - 1, i == N - 1 ? lane - N + 1 : lane + 1};
+    const int64_t f_first = wave * c.fpw;
+    const int64_t f_left = c.F - f_first;
+    const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
+    float rsum = 0.f, dsum = 0.f;
+    // every wave runs its body (each holds one barrier), also the waves with no formation
+    if (w8 < 4)
+        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleState>(
+            c, st, p, x, active, f, a, i, nullptr, lane, M, f_first * N, T, act, gen, nullptr,
+            rew, done, rsum, dsum);
+    else
+        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObs>(
+            c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N, T, act, gen, obs,
+            nullptr, nullptr, rsum, dsum);
+    if (partial) {
+        if (w8 < 4) {
+            rsum = wave_sum(rsum);
+            dsum = wave_sum(dsum);
+            if (lane == 0) red[w] = make_float2(rsum, dsum);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float2 v = red[0];
+            for (int k = 1; k < 4; ++k) v = make_float2(v.x + red[k].x, v.y + red[k].y);
             if (accum) v = make_float2(partial[blockIdx.x].x + v.x, partial[blockIdx.x].y + v.y);
             partial[blockIdx.x] = v;
         }
@@ -632,6 +700,16 @@ static inline bool use_pf(const Consts &c, int32_t T) {
     return FENV_SMALL_PF > 1 && T >= FENV_SMALL_PF && waves < FENV_RS_MIN_WAVES;
 }
 
+// Small latency-bound grids: the role-split kernel (two waves per formation-wave, see
+// k_rollout_wave_split) where the grid leaves most SIMDs idle.  FENV_SPLIT=0 turns it off (A/B).
+#ifndef FENV_SPLIT
+#define FENV_SPLIT 1
+#endif
+static inline bool use_split(const Consts &c) {
+    const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
+    return FENV_SPLIT && wave_path(c.N) && waves < FENV_RS_MIN_WAVES;
+}
+
 int64_t rollout_group_count(const Consts &c) {
 #if FENV_RW
     if (wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
@@ -679,6 +757,14 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
         hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
                            dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
                            a2, g0, obs, rew, done, p2, accum);
+    } else if (use_split(c)) {
+        const unsigned blocks = (unsigned)group_count(c);
+        if (use_pf(c, T))
+            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, FENV_SMALL_PF>), dim3(blocks),
+                               dim3(512), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
+        else
+            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, 1>), dim3(blocks), dim3(512),
+                               0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
         if (use_pf(c, T))
@@ -700,6 +786,8 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
     if (wave_path(c.N)) return "k_rollout_wg";
 #endif
     if (use_rs(c, T)) return "k_rollout_wave_rs";
+    if (use_split(c))
+        return use_pf(c, T) ? "k_rollout_wave_split (prefetch 4)" : "k_rollout_wave_split";
     if (wave_path(c.N)) return use_pf(c, T) ? "k_rollout_wave (prefetch 4)" : "k_rollout_wave";
     return "k_rollout_block";
 }
