@@ -484,12 +484,14 @@ def main():
             nstat[0] += 1
 
     def region(plan, stat_every, evs=None):
-        """The timed region's work: the launches of `plan`, stats every `stat_every` launches,
-        then the wait for the stats (side stream / all-reduce)."""
+        """The timed region's work: the launches of `plan`, stats on the first launch of every
+        `stat_every` (so a region of several launches never ends on a stats reduction: it runs
+        on the side stream under the next launch), then the wait for the stats (side stream /
+        all-reduce)."""
         if evs is not None:
             evs[0].record(main_s)
         for k, L in enumerate(plan):
-            launch(L, stat=not args.no_stats and (k + 1) % stat_every == 0,
+            launch(L, stat=not args.no_stats and k % stat_every == 0,
                    last=k == len(plan) - 1)
             if evs is not None:
                 evs[k + 1].record(main_s)
@@ -603,7 +605,8 @@ def main():
             out["roofline"]["same_box_ceiling"] = ceiling
         if not args.no_stats:
             t = tot.cpu().tolist()
-            out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * plan[-1]),
+            sampled = [L for k, L in enumerate(plan) if k % stat_every == 0][-1]
+            out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * sampled),
                                     "agent_dones_sampled_rollout": t[1],
                                     "every_launches": stat_every}
         if world == 1 and not args.no_policy:
