@@ -49,6 +49,11 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
 #ifndef FENV_RS_XCD
 #define FENV_RS_XCD 0
 #endif
+// Occupancy probe (FENV_RS_PAD bytes of extra LDS per workgroup caps the resident workgroups per
+// CU: A/B builds only, 0 in the product).
+#ifndef FENV_RS_PAD
+#define FENV_RS_PAD 0
+#endif
 __device__ __forceinline__ int64_t xcd_slice(int64_t b, int64_t nb) {
     if (!FENV_RS_XCD) return b;
     const int64_t x = b & 7, q = nb >> 3, r = nb & 7;
@@ -329,6 +334,10 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     __shared__ __attribute__((aligned(16))) float rbuf[kRSTB * kRSA];
     __shared__ __attribute__((aligned(16))) uint8_t dbuf[kRSTB * kRSA];
     __shared__ float2 red[kRS];
+#if FENV_RS_PAD > 0
+    __shared__ char rs_pad[FENV_RS_PAD];
+    if (T < 0) rs_pad[threadIdx.x] = 0;  // never taken (T >= 0): keeps the allocation
+#endif
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t blk = xcd_slice(blockIdx.x, gridDim.x);
     const int64_t wave = blk * kRS + w;

@@ -14,8 +14,11 @@
 // every epoch inside one launch.  The 64-deep contractions (layer 2 forward, W2 gradients,
 // dL/dh1, W1 gradients) run on the fp32 MFMA pipe (v_mfma_f32_32x32x2f32 / 16x16x4f32: exact
 // fp32 products, fp32 accumulation); the parameter and gradient images are padded (lx) so the
-// operand reads are bank-conflict free.  Results match the torch path to summation-order
-// rounding (tests/test_gpu_rollout.py).
+// operand reads are bank-conflict free, and the two 32-step MFMA loops keep the LDS reads of
+// step i + 8 in flight under the MFMAs of step i (an explicit register ring).  tanh is
+// 1 - 2 / (1 + e^2x) on v_exp/v_rcp and the gradient norm is summed by the threads that write
+// the gradient entries.  Results match the torch path to summation-order rounding plus the
+// tanh's < 3e-7 (tests/test_gpu_rollout.py).
 //
 // Work split per minibatch (B <= 64 samples, 8 waves, 2 per SIMD); every contraction runs over
 // all 64 sample rows (rows >= B hold finite stale values and are multiplied by zeroed dL/dz):
@@ -27,7 +30,8 @@
 //   backward head weight grads (16x16x4 tile of hidden rows per wave) and dL/dz2 in place of the
 //            same wave's H2 columns (rows >= B zeroed); one 32 x 32 tile of both W2 grads and
 //            dL/dh1 per wave, dL/dz1 in place of layer 1 after a barrier; W1 grads (16x16x4).
-//   update   global grad 2-norm (block reduction), clip, Adam with bias correction.
+//   update   global grad 2-norm (per-thread sums of the entries each wrote, block reduction), clip,
+//            Adam with bias correction.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -80,12 +84,40 @@ struct PPOArgs {
     double *stats;
 };
 
+// tanh x = 1 - 2 / (1 + e^(2x)) on v_exp_f32 + v_rcp_f32 (absolute error < 3e-7 over the whole
+// range, +-1 at +-inf) instead of the ~30-instruction libm tanhf: the update's forward only has
+// to match torch's tanh to fp32 rounding noise (tests/test_gpu_rollout.py bounds the update)
+#ifndef FENV_PPO_FAST_TANH
+#define FENV_PPO_FAST_TANH 1
+#endif
+__device__ __forceinline__ float tanh_u(float x) {
+#if FENV_PPO_FAST_TANH
+    const float e = __builtin_amdgcn_exp2f(x * 2.88539008177792681f);  // 2 log2(e)
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+#else
+    return tanhf(x);
+#endif
+}
+
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     return v;
 }
 
+// unroll of the two 32-step fp32 MFMA loops (layer-2 forward; W2 grads + dL/dh1)
+#ifndef FENV_PPO_UL2
+#define FENV_PPO_UL2 8
+#endif
+#ifndef FENV_PPO_U2
+#define FENV_PPO_U2 4
+#endif
+#ifndef FENV_PPO_RING
+#define FENV_PPO_RING 8  // > 0: W2-grad loop with an explicit operand ring of this depth
+#endif
+#ifndef FENV_PPO_RING_L2
+#define FENV_PPO_RING_L2 8  // > 0: the same for the layer-2 forward loop
+#endif
 #ifndef FENV_PPO_DUMP_GRAD
 #define FENV_PPO_DUMP_GRAD 0
 #endif
@@ -177,6 +209,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
         for (int64_t s0 = 0; s0 < n; s0 += bs, ++kmb) {
             const int B = (int)((n - s0) < bs ? (n - s0) : bs);
             const float invB = 1.0f / (float)B;
+            float gss = 0.f;  // sum of squares of the gradient entries this thread writes
             // ---- gather the minibatch (from the prefetch registers), then start the next one
             if (tid < B * 8) O[(tid >> 3) * 9 + (tid & 7)] = po;
             if (tid < B) {
@@ -215,7 +248,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[4], b1, acc, 0, 0, 0);
                     float *hr = H1 + (net * kPB + 16 * bt + 4 * q) * kRow + j;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) hr[r * kRow] = tanhf(acc[r]);
+                    for (int r = 0; r < 4; ++r) hr[r * kRow] = tanh_u(acc[r]);
                 }
             }
             __syncthreads();
@@ -232,12 +265,33 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
-#pragma unroll 8
+#if FENV_PPO_RING_L2
+                constexpr int RL = FENV_PPO_RING_L2;
+                float ra[RL], rb[RL];
+#pragma unroll
+                for (int j = 0; j < RL; ++j) {
+                    ra[j] = Ar[j];
+                    rb[j] = Bc[j];
+                }
+#pragma unroll
+                for (int i0 = 0; i0 < 32; i0 += RL) {
+#pragma unroll
+                    for (int j = 0; j < RL; ++j) {
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], acc, 0, 0, 0);
+                        if (i0 + RL + j < 32) {
+                            ra[j] = Ar[i0 + RL + j];
+                            rb[j] = Bc[i0 + RL + j];
+                        }
+                    }
+                }
+#else
+#pragma unroll FENV_PPO_UL2
                 for (int i = 0; i < 32; ++i)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ar[i], Bc[i], acc, 0, 0, 0);
+#endif
                 float *Hr = H2 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) Hr[rho(r, h) * kRow] = tanhf(acc[r]);
+                for (int r = 0; r < 16; ++r) Hr[rho(r, h) * kRow] = tanh_u(acc[r]);
             }
             __syncthreads();
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
@@ -318,11 +372,13 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     st_el += (double)(-ent);
                     st_cf += (double)(cf * invB);
                     // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls = 1)
-                    G[lx(L.logstd)] = gls0 - hp.ent_coef;
-                    G[lx(L.logstd + 1)] = gls1 - hp.ent_coef;
+                    const float g0 = gls0 - hp.ent_coef, g1 = gls1 - hp.ent_coef;
+                    G[lx(L.logstd)] = g0;
+                    G[lx(L.logstd + 1)] = g1;
                     G[lx(L.actb)] = sgmu0;
                     G[lx(L.actb + 1)] = sgmu1;
                     G[lx(L.valb)] = sgv;
+                    gss = g0 * g0 + g1 * g1 + sgmu0 * sgmu0 + sgmu1 * sgmu1 + sgv * sgv;
                 }
             }
             __syncthreads();
@@ -347,7 +403,10 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 if (c < ncol) {
                     const int hw = net ? L.valW : L.actW + c * kHid;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) G[lx(hw + 16 * kt + 4 * q + r)] = acc[r];
+                    for (int r = 0; r < 4; ++r) {
+                        G[lx(hw + 16 * kt + 4 * q + r)] = acc[r];
+                        gss = __builtin_fmaf(acc[r], acc[r], gss);
+                    }
                 }
                 const int k = 16 * kt + c;
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
@@ -382,7 +441,38 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 f32x16 gw, dz;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) gw[r] = dz[r] = 0.0f;
-#pragma unroll 4
+#if FENV_PPO_RING
+                // operands of step i + RD loaded while steps i.. issue (RD-deep register ring)
+                constexpr int RD = FENV_PPO_RING;
+                const float *pa = Z2 + (32 * h) * kRow + 32 * mt + c;
+                const float *pb = A1 + (32 * h) * kRow + 32 * nt + c;
+                const float *pc = Z2 + (32 * mt + c) * kRow + 32 * h;
+                const float *pd = W + w2 + (32 * h) * kRow + 32 * nt + c;
+                float ra[RD], rb[RD], rc[RD], rd[RD];
+#pragma unroll
+                for (int j = 0; j < RD; ++j) {
+                    ra[j] = pa[j * kRow];
+                    rb[j] = pb[j * kRow];
+                    rc[j] = pc[j];
+                    rd[j] = pd[j * kRow];
+                }
+#pragma unroll
+                for (int i0 = 0; i0 < 32; i0 += RD) {
+#pragma unroll
+                    for (int j = 0; j < RD; ++j) {
+                        gw = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], gw, 0, 0, 0);
+                        dz = __builtin_amdgcn_mfma_f32_32x32x2f32(rc[j], rd[j], dz, 0, 0, 0);
+                        const int i = i0 + RD + j;
+                        if (i < 32) {
+                            ra[j] = pa[i * kRow];
+                            rb[j] = pb[i * kRow];
+                            rc[j] = pc[i];
+                            rd[j] = pd[i * kRow];
+                        }
+                    }
+                }
+#else
+#pragma unroll FENV_PPO_U2
                 for (int i = 0; i < 32; ++i) {
                     const int kk = 32 * h + i;
                     gw = __builtin_amdgcn_mfma_f32_32x32x2f32(Z2[kk * kRow + 32 * mt + c],
@@ -391,9 +481,13 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                                                              W[w2 + kk * kRow + 32 * nt + c], dz,
                                                              0, 0, 0);
                 }
+#endif
                 float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) Gr[rho(r, h) * kRow] = gw[r];
+                for (int r = 0; r < 16; ++r) {
+                    Gr[rho(r, h) * kRow] = gw[r];
+                    gss = __builtin_fmaf(gw[r], gw[r], gss);
+                }
                 if (tid < 2 * kHid) {
                     const int bn = tid >> 6, j = tid & 63;
                     const float *z2 = H2 + bn * kPB * kRow + j;
@@ -401,6 +495,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll 8
                     for (int b = 0; b < B; ++b) acc += z2[b * kRow];
                     G[lx((bn ? L.vf2b : L.pi2b) + j)] = acc;
+                    gss = __builtin_fmaf(acc, acc, gss);
                 }
                 __syncthreads();
                 FENV_PPO_PHASE(6);
@@ -430,7 +525,10 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 if (c < D) {
                     const int w1 = (net ? L.vf0W : L.pi0W) + (16 * jt + 4 * q) * D + c;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) G[lx(w1 + r * D)] = acc[r];
+                    for (int r = 0; r < 4; ++r) {
+                        G[lx(w1 + r * D)] = acc[r];
+                        gss = __builtin_fmaf(acc[r], acc[r], gss);
+                    }
                 }
             }
             if (tid < 2 * kHid) {
@@ -440,19 +538,15 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll 8
                 for (int b = 0; b < B; ++b) acc += z1[b * kRow];
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
+                gss = __builtin_fmaf(acc, acc, gss);
             }
+            // ---- clip_grad_norm_(max_grad_norm): global 2-norm from the squares each thread
+            // accumulated as it wrote its gradient entries (every entry is written exactly once
+            // per minibatch), one wave sum each, reduced after the barrier
+            gss = wsum(gss);
+            if (lane == 0) R[w] = gss;
             __syncthreads();
             FENV_PPO_PHASE(8);
-            // ---- clip_grad_norm_(max_grad_norm): global 2-norm
-            float ss = 0.f;
-#pragma unroll
-            for (int q = 0; q < kPerT; ++q) {
-                const int p = tid + q * kPT;
-                if (p < P) ss = __builtin_fmaf(G[lx(p)], G[lx(p)], ss);
-            }
-            ss = wsum(ss);
-            if (lane == 0) R[w] = ss;
-            __syncthreads();
             FENV_PPO_PHASE(9);
             float tot = 0.f;
             for (int q = 0; q < kPT / 64; ++q) tot += R[q];
