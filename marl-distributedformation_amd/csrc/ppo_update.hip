@@ -99,6 +99,34 @@ __device__ __forceinline__ float tanh_u(float x) {
 #endif
 }
 
+#ifndef FENV_PPO_UDZ
+#define FENV_PPO_UDZ 4  // unroll of the dL/dz2 loop (16 steps)
+#endif
+#ifndef FENV_PPO_BSUM4
+#define FENV_PPO_BSUM4 1  // bias-gradient column sums over all kPB rows in 4 partial sums (0: B rows, one chain)
+#endif
+// Column sum of an activation-gradient image (rows at stride kRow): the bias gradient.  Rows
+// b >= B of dL/dz2 and dL/dz1 are exact zeros, so summing all kPB rows adds only zeros.
+__device__ __forceinline__ float col_sum(const float *z, int B) {
+#if FENV_PPO_BSUM4
+    (void)B;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int b = 0; b < kPB; b += 4) {
+        a0 += z[b * kRow];
+        a1 += z[(b + 1) * kRow];
+        a2 += z[(b + 2) * kRow];
+        a3 += z[(b + 3) * kRow];
+    }
+    return (a0 + a1) + (a2 + a3);
+#else
+    float acc = 0.f;
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) acc += z[b * kRow];
+    return acc;
+#endif
+}
+
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
@@ -411,7 +439,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 const int k = 16 * kt + c;
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
                 const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
-#pragma unroll 4
+#pragma unroll FENV_PPO_UDZ
                 for (int t = 0; t < 16; ++t) {
                     const int b = 4 * t + q;
                     float *hp2 = hcol + b * kRow + c;
@@ -491,9 +519,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 if (tid < 2 * kHid) {
                     const int bn = tid >> 6, j = tid & 63;
                     const float *z2 = H2 + bn * kPB * kRow + j;
-                    float acc = 0.f;
-#pragma unroll 8
-                    for (int b = 0; b < B; ++b) acc += z2[b * kRow];
+                    const float acc = col_sum(z2, B);
                     G[lx((bn ? L.vf2b : L.pi2b) + j)] = acc;
                     gss = __builtin_fmaf(acc, acc, gss);
                 }
@@ -534,9 +560,7 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             if (tid < 2 * kHid) {
                 const int net = tid >> 6, j = tid & 63;
                 const float *z1 = H1 + net * kPB * kRow + j;
-                float acc = 0.f;
-#pragma unroll 8
-                for (int b = 0; b < B; ++b) acc += z1[b * kRow];
+                const float acc = col_sum(z1, B);
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
                 gss = __builtin_fmaf(acc, acc, gss);
             }
