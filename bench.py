@@ -527,6 +527,11 @@ def main():
     for _ in range(more):
         pw_ms += prewarm_region()
         pw_launches += 5
+    # the timed region's plan and events are made before the closing synchronize, so nothing but
+    # the barrier separates the warm-up launches from the first timed launch
+    plan = launch_plan(args.steps, T)
+    stat_every = max(1, min(args.stats_every, len(plan)))
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
     for L in launch_plan(args.warmup, T):
         launch(L)
     torch.cuda.synchronize()
@@ -534,9 +539,6 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
 
-    plan = launch_plan(args.steps, T)
-    stat_every = max(1, min(args.stats_every, len(plan)))
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
     t0 = time.perf_counter()
     tot = region(plan, stat_every, evs)
     t_issued = time.perf_counter() - t0
@@ -595,6 +597,7 @@ def main():
                          "avg_kernel_ms": kern_avg_ms, "kernel_ms_timed": kern_total_ms,
                          "launches": len(plan),
                          "launch_ms_min": min(per_launch), "launch_ms_max": max(per_launch),
+                         "launch_ms_first": per_launch[:8],
                          "timing": "HIP events on the launch stream at every launch boundary"},
         }
         if ceiling is not None:

@@ -274,10 +274,27 @@ __device__ __forceinline__ void store_obs_rows(float *stage, const float (&o)[8]
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef FENV_WAVE_SUM_DPP
+#define FENV_WAVE_SUM_DPP 1
+#endif
+// Sum over the 64 lanes, returned in every lane.  DPP form: row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast 15 / 31 carry the row sums up, so lane 63 holds the total (a fixed order:
+// deterministic), read back with v_readlane.  Six VALU ops instead of six LDS-latency swizzles.
 __device__ __forceinline__ float wave_sum(float v) {
+#if FENV_WAVE_SUM_DPP
+    int x = __float_as_int(v);
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+#else
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     return v;
+#endif
 }
 
 }  // namespace fenvk
