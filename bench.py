@@ -115,6 +115,22 @@ def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
             "reference_measured": REFERENCE_CPU_MEASURED}
 
 
+def _warm(fn, min_ms: float = 300.0) -> int:
+    """Run `fn` back to back for at least `min_ms` of wall time, then synchronize: each
+    secondary line starts from the clocks a sustained load holds (a few warm-up calls after an
+    idle gap left the fused policy rollout ~15 % slow, tools/collect_overhead.py).  Returns the
+    number of calls."""
+    import torch
+    n, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < min_ms or n < 3:
+        fn()
+        n += 1
+        if n % 64 == 0:
+            torch.cuda.synchronize()  # bounds the queue (short kernels issue faster than they run)
+    torch.cuda.synchronize()
+    return n
+
+
 def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollouts: int) -> dict:
     """Secondary measurement (BASELINE config 2): on-device PPO rollout collection with the MFMA
     policy forward + env step per step (65536 formations x 10 agents), plus the policy
@@ -130,9 +146,7 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
     pol = pol_mod.MlpPolicy(8, device=dev, seed=0)
     buf = ro.RolloutBuffer(10, A, 8, dev)
     col = ro.RolloutCollector(env, pol, buf, seed=0)
-    for _ in range(2):
-        col.collect()
-    torch.cuda.synchronize()
+    _warm(col.collect)
     t0 = time.perf_counter()
     for _ in range(rollouts):
         col.collect()
@@ -145,6 +159,7 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
                 last_done=col.last_episode_starts, last_obs=col.last_obs,
                 last_value=col._last_values)
     ka, kb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _warm(lambda: env.policy_rollout(pol.flat, 10, bufs, seed=0, offset=500), 100.0)
     ka.record()
     for r in range(rollouts):
         env.policy_rollout(pol.flat, 10, bufs, seed=0, offset=1000 + 10 * r)
@@ -157,6 +172,7 @@ def policy_rollout_bench(pkgname: str, dev, formations: int, agents: int, rollou
                log_prob=buf.log_probs[0], clipped=buf.clipped[0])
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(20)]
+    _warm(lambda: pol.forward(obs, out=out, seed=0, offset=0), 100.0)
     for a, b in evs:
         a.record()
         pol.forward(obs, out=out, seed=0, offset=0)
@@ -224,9 +240,7 @@ def env_config_bench(pkgname: str, dev, formations: int, agents: int, launches: 
     rew = torch.empty((T, A), device=dev)
     done = torch.empty((T, A), dtype=torch.bool, device=dev)
     env.reset_tensor()
-    for _ in range(3):
-        env.rollout(acts, obs, rew, done)
-    torch.cuda.synchronize()
+    _warm(lambda: env.rollout(acts, obs, rew, done), 200.0)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     a.record()
@@ -260,9 +274,7 @@ def random_action_bench(pkgname: str, dev, formations: int, agents: int, launche
     rew = torch.empty((T, A), device=dev)
     done = torch.empty((T, A), dtype=torch.bool, device=dev)
     env.reset_tensor()
-    for k in range(3):
-        env.rollout_random(T, 7, k * T, obs, rew, done)
-    torch.cuda.synchronize()
+    _warm(lambda: env.rollout_random(T, 7, 0, obs, rew, done), 200.0)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     a.record()
