@@ -54,7 +54,10 @@ enum {
  * (sharding; pass 0 and num_formation for an unsharded env).  Like the reference ctor it
  * consumes the first reset draw set (simulate.py:61).  share_reward_ratio is the simulator's
  * (simulate.py:11; the reference env never forwards its cfg key, so pass 0.25 for parity).
- * Formation sizes: 1 <= num_agents <= 1024. */
+ * Formation sizes: 1 <= num_agents <= FENV_MAX_AGENTS (the reference takes any size; up to 64
+ * agents a wavefront holds whole formations, up to 1024 a workgroup holds one formation, larger
+ * formations run several agents per thread with the exchanges through global scratch). */
+#define FENV_MAX_AGENTS (1 << 24)
 int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num_agents,
                 int32_t goal_in_obs, double share_reward_ratio, int32_t max_steps, uint32_t seed,
                 int32_t reset_mode, int64_t first_formation, int64_t total_formations);

@@ -64,13 +64,16 @@ def load_config(path: str | None = None, overrides: Iterable[str] = ()) -> Confi
     return cfg
 
 
+MAX_AGENTS = 1 << 24  # include/fenv.h FENV_MAX_AGENTS
+
+
 def validate(cfg) -> None:
     F = int(getattr(cfg, "num_formation"))
     N = int(getattr(cfg, "num_agents_per_formation"))
     if F < 1:
         raise ValueError("num_formation must be >= 1")
-    if not 1 <= N <= 1024:
-        raise ValueError("num_agents_per_formation must be in [1, 1024]")
+    if not 1 <= N <= MAX_AGENTS:
+        raise ValueError(f"num_agents_per_formation must be in [1, {MAX_AGENTS}]")
     s = float(getattr(cfg, "share_reward_ratio", 0.25))
     if not 0.0 <= s <= 0.5:
         raise ValueError("share_reward_ratio must be in [0, 0.5] (simulate.py:28)")

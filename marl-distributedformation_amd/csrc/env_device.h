@@ -92,8 +92,12 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
 }
 
 // ---------------------------------------------------------------- ring-neighbour exchange
-// Four exchange rounds per env step: A {px,py}->next, B {drr}->prev, C {ind}->prev,next,
-// D {nx,ny}->prev,next.
+// Three exchange rounds per env step: A {px,py}->prev,next, C {ind}->prev,next, D {nx,ny}->
+// prev,next.  FENV_XA=0 (A/B builds) restores round 1's four: A {px,py}->next, B {drr}->prev
+// (the left distance taken as the right distance of agent i-1), C, D.
+#ifndef FENV_XA
+#define FENV_XA 1
+#endif
 
 struct WaveX {  // N <= 64: lanes of one formation are contiguous in the wavefront
     int lp, ln;
@@ -102,6 +106,13 @@ struct WaveX {  // N <= 64: lanes of one formation are contiguous in the wavefro
         vn = __shfl(v, ln, 64);
     }
     __device__ __forceinline__ float b_prev(float v) const { return __shfl(v, lp, 64); }
+    __device__ __forceinline__ void a_pn(float u, float v, float &up, float &un, float &vp,
+                                         float &vn) const {
+        up = __shfl(u, lp, 64);
+        un = __shfl(u, ln, 64);
+        vp = __shfl(v, lp, 64);
+        vn = __shfl(v, ln, 64);
+    }
     __device__ __forceinline__ void c_pn(float v, float &vp, float &vn) const {
         vp = __shfl(v, lp, 64);
         vn = __shfl(v, ln, 64);
@@ -118,7 +129,8 @@ struct WaveX {  // N <= 64: lanes of one formation are contiguous in the wavefro
 constexpr int kMaxN = 1024;
 
 // N > 64: one formation per workgroup, slots in LDS.  Each slot's next write is separated from
-// its previous reads by at least one barrier (rounds are used in the order A,B,C,D).
+// its previous reads by at least one barrier (rounds are used in the order A,[B,]C,D; A and a_pn
+// share slots 0-1).
 struct BlockX {
     float *lds;  // 6 * kMaxN floats
     int i, ip, in;
@@ -127,6 +139,16 @@ struct BlockX {
         lds[1 * kMaxN + i] = v;
         __syncthreads();
         un = lds[0 * kMaxN + in];
+        vn = lds[1 * kMaxN + in];
+    }
+    __device__ __forceinline__ void a_pn(float u, float v, float &up, float &un, float &vp,
+                                         float &vn) const {
+        lds[0 * kMaxN + i] = u;
+        lds[1 * kMaxN + i] = v;
+        __syncthreads();
+        up = lds[0 * kMaxN + ip];
+        un = lds[0 * kMaxN + in];
+        vp = lds[1 * kMaxN + ip];
         vn = lds[1 * kMaxN + in];
     }
     __device__ __forceinline__ float b_prev(float v) const {
@@ -176,10 +198,19 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
 
     // compute_reward_and_done, simulate.py:180-211
     const float dg = norm2(s.px - s.gx, s.py - s.gy);
+#if FENV_XA
+    // one exchange round for both neighbours' positions; both distances computed here as the
+    // reference does (:197-198: norm(p - roll(p, -1)), norm(p - roll(p, 1)))
+    float ppx, pnx, ppy, pny;
+    x.a_pn(s.px, s.py, ppx, pnx, ppy, pny);
+    const float drr = norm2(s.px - pnx, s.py - pny);  // ||p_i - p_{i+1}||  (:197)
+    const float drl = norm2(s.px - ppx, s.py - ppy);  // ||p_i - p_{i-1}||  (:198)
+#else
     float pnx, pny;
     x.a_next(s.px, s.py, pnx, pny);
     const float drr = norm2(s.px - pnx, s.py - pny);  // ||p_i - p_{i+1}||  (:197)
     const float drl = x.b_prev(drr);                  // ||p_i - p_{i-1}|| == drr_{i-1} bitwise
+#endif
     const float ctg = dg < 100.0f ? 10.0f : 0.0f;     // :183-187
     const float rd = -0.1f * dg;                      // :191
     const float rr = nb_reward(drr - c.d_nb);         // :202-205

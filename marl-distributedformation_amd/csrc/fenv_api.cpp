@@ -69,12 +69,13 @@ struct fenv {
     float *term = nullptr;   // device: terminal (px, py, gx, gy)[A] of the latest done step
     bool term_valid = false; // last state-changing call was a step (t == 0 <=> reset by it)
     float *lv_scratch = nullptr;  // last values for GAE when the caller passes none
+    float *lf = nullptr;     // device: large-formation exchange scratch (N > 1024 only)
     std::mt19937 mt;         // the reference's global stream (all formations of all shards)
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
 
     size_t pend_floats() const { return (size_t)(2 * A + 2 * c.F); }
     fenvk::DevPending pending() const {
-        return fenvk::DevPending{pend, reinterpret_cast<float4 *>(term)};
+        return fenvk::DevPending{pend, reinterpret_cast<float4 *>(term), lf};
     }
 
     // A launch that may read the staged set waits (on the device) for its latest refill, which
@@ -134,8 +135,8 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     if (!out) return fail(FENV_EINVAL, "fenv_create: out is NULL");
     *out = nullptr;
     if (num_formation < 1) return fail(FENV_EINVAL, "num_formation must be >= 1");
-    if (num_agents < 1 || num_agents > 1024)
-        return fail(FENV_EINVAL, "num_agents_per_formation must be in [1, 1024]");
+    if (num_agents < 1 || num_agents > FENV_MAX_AGENTS)
+        return fail(FENV_EINVAL, "num_agents_per_formation must be in [1, FENV_MAX_AGENTS]");
     if (!(share_reward_ratio >= 0.0 && share_reward_ratio <= 0.5))
         return fail(FENV_EINVAL, "share_reward_ratio must be in [0, 0.5] (simulate.py:28)");
     if (max_steps < 0) return fail(FENV_EINVAL, "max_steps must be >= 0");
@@ -195,6 +196,10 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(terminal state) failed"));
     he = hipMemset(e->term, 0, 4 * A * sizeof(float));
     if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipMemset(terminal state) failed"));
+    if (fenvk::large_path(num_agents)) {
+        he = hipMalloc(&e->lf, fenvk::kLargeScratchPerAgent * A * sizeof(float));
+        if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(exchange scratch) failed"));
+    }
     if (reset_mode == FENV_RESET_MT19937) {
         he = hipMalloc(&e->pend, e->pend_floats() * sizeof(float));
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
@@ -224,6 +229,7 @@ int fenv_destroy(fenv_t *e) {
     if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
     if (e->lv_scratch) (void)hipFree(e->lv_scratch);
     if (e->term) (void)hipFree(e->term);
+    if (e->lf) (void)hipFree(e->lf);
     delete e;
     return FENV_OK;
 }

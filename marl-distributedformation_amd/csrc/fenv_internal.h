@@ -27,6 +27,8 @@ struct DevPending {
     const float *pend;  // staged draw set px[A] py[A] gx[F] gy[F] (NULL in Philox mode)
     float4 *term;       // terminal (px, py, gx, gy)[A] (the goal repeated per agent: one
                         // store, one index)
+    float *lf;          // N > kMaxN only: per-agent exchange scratch of the large-formation
+                        // kernels (fenv_large.hip), 7 x [A] floats; NULL otherwise
 };
 
 struct Consts {
@@ -41,9 +43,14 @@ struct Consts {
     uint32_t key0, key1;// Philox key
 };
 
-// Geometry: N <= 64 -> `fpw` whole formations per wavefront, 256-thread workgroups.
-//           N  > 64 -> one formation per workgroup of round_up(N, 64) threads (LDS exchange).
+// Geometry: N <= 64   -> `fpw` whole formations per wavefront, 256-thread workgroups.
+//           N <= 1024 -> one formation per workgroup of round_up(N, 64) threads (LDS exchange).
+//           N  > 1024 -> one formation per 1024-thread workgroup, several agents per thread,
+//                        exchanges through global scratch (fenv_large.hip).
 inline bool wave_path(int32_t N) { return N <= 64; }
+constexpr int32_t kBlockMaxN = 1024;
+inline bool large_path(int32_t N) { return N > kBlockMaxN; }
+constexpr int kLargeScratchPerAgent = 7;  // floats of DevPending::lf per agent
 int64_t group_count(const Consts &c);  // 4-wave workgroups (N<=64) or formations (N>64)
 // workgroups of the rollout/step launch = records of its stats partials
 int64_t rollout_group_count(const Consts &c);
@@ -69,6 +76,15 @@ constexpr int kMetricCols = 8;
 hipError_t launch_metrics(const Consts &c, const DevState &s, const DevPending &p, bool terminal,
                           const float *rew, float *out, double *sums, hipStream_t st);
 const char *rollout_kernel_name(const Consts &c, int32_t T);
+// large formations (large_path(N)): the same entry points' kernels, fenv_large.hip
+hipError_t launch_rollout_large(const Consts &c, const DevState &s, const DevPending &p,
+                                int32_t T, int32_t D, const float *act, float *obs, float *rew,
+                                uint8_t *done, float *partial, bool accumulate, hipStream_t st,
+                                const ActGen *gen);
+hipError_t launch_reset_observe_large(const Consts &c, const DevState &s, const DevPending &p,
+                                      int32_t D, bool do_reset, float *obs, hipStream_t st);
+hipError_t launch_metrics_large(const Consts &c, const DevState &s, const DevPending &p,
+                                bool terminal, const float *rew, float *out, hipStream_t st);
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st);
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,

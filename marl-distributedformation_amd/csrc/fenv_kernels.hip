@@ -794,6 +794,7 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
 #if FENV_RW
     if (wave_path(c.N)) return "k_rollout_wg";
 #endif
+    if (large_path(c.N)) return "k_rollout_large";
     if (use_rs(c, T)) return "k_rollout_wave_rs";
     if (use_split(c))
         return use_pf(c, T) ? "k_rollout_wave_split (prefetch 4)" : "k_rollout_wave_split";
@@ -804,6 +805,8 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
                           float *partial, bool accum, hipStream_t st, const ActGen *gen) {
+    if (large_path(c.N))
+        return launch_rollout_large(c, s, p, T, D, act, obs, rew, done, partial, accum, st, gen);
     const bool mt = c.reset_mode == FENV_RESET_MT19937;
     if (D == 8)
         return mt ? rollout_dm<8, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial,
@@ -840,13 +843,17 @@ static hipError_t reset_obs_d(const Consts &c, const DevState &s, const DevPendi
 
 hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPending &p,
                                 int32_t D, bool do_reset, float *obs, hipStream_t st) {
+    if (large_path(c.N)) return launch_reset_observe_large(c, s, p, D, do_reset, obs, st);
     return D == 8 ? reset_obs_d<8>(c, s, p, do_reset, obs, st)
                   : reset_obs_d<6>(c, s, p, do_reset, obs, st);
 }
 
 hipError_t launch_metrics(const Consts &c, const DevState &s, const DevPending &p, bool terminal,
                           const float *rew, float *out, double *sums, hipStream_t st) {
-    if (wave_path(c.N)) {
+    if (large_path(c.N)) {
+        hipError_t e = launch_metrics_large(c, s, p, terminal, rew, out, st);
+        if (e != hipSuccess) return e;
+    } else if (wave_path(c.N)) {
         hipLaunchKernelGGL(k_metrics_wave, dim3((unsigned)group_count(c)), dim3(256), 0, st, c,
                            s, p, terminal, rew, out);
     } else {

@@ -39,7 +39,7 @@ def test_signatures_cover_header(flib):
     assert set(flib.header_symbols()) <= set(flib.SIGNATURES)
 
 
-@pytest.mark.parametrize("N", [1, 2, 3, 5, 7, 10, 64, 100, 1024])
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 7, 10, 64, 100, 1024, 1025, 5000, 1 << 24])
 def test_desired_neighbor_dist(flib, N):
     assert np.float32(flib.lib().fenv_desired_neighbor_dist(N)) == desired_neighbor_dist(N)
 
@@ -195,3 +195,16 @@ print("ok")
 """ % ROOT
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+
+
+def test_formation_size_limits(pkg):
+    """Any formation size the reference takes up to include/fenv.h's FENV_MAX_AGENTS (2^24) is
+    accepted by the config layer (large formations run fenv_large.hip's kernels); 0 and larger
+    sizes are rejected before anything is allocated."""
+    from importlib import import_module
+    cfgm = import_module(pkg.__name__ + ".config")
+    for N in (1, 64, 1024, 1025, 5000, 1 << 24):
+        cfgm.validate(cfgm.as_config({"num_formation": 2, "num_agents_per_formation": N}))
+    for N in (0, (1 << 24) + 1):
+        with pytest.raises(ValueError):
+            cfgm.validate(cfgm.as_config({"num_formation": 2, "num_agents_per_formation": N}))

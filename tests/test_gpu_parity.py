@@ -140,7 +140,9 @@ def run_vs_oracle(venv, F, N, goal, seed, steps, chunks, amp=1.2, max_steps=1000
 
 
 @pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 7, 10, 12, 21, 32, 33, 63, 64, 65, 100, 128, 257,
-                               1000, 1024])
+                               1000, 1024,
+                               # several agents per thread (k_rollout_large, fenv_large.hip)
+                               1025, 1500, 2048, 3001])
 def test_all_formation_sizes_vs_oracle(venv, N):
     F = max(3, 1200 // N)
     run_vs_oracle(venv, F, N, True, 100 + N, steps=60, chunks=[1, 5, 23], max_steps=17)
@@ -193,7 +195,7 @@ def test_out_of_bounds_heavy(venv):
     run_vs_oracle(venv, 200, 5, True, 5, steps=120, chunks=[13], amp=40.0, max_steps=50)
 
 
-@pytest.mark.parametrize("F,N", [(24581, 5), (12, 100), (9, 1024), (301, 1)])
+@pytest.mark.parametrize("F,N", [(24581, 5), (12, 100), (9, 1024), (301, 1), (3, 1500)])
 def test_extreme_actions_vs_oracle(venv, F, N):
     """Unclipped edge-case actions (signed zeros, subnormal, huge, ±inf; oracle.EXTREME_ACTIONS,
     pinned against the reference by the *_extreme fixtures) through the staged wave kernel, the
@@ -271,8 +273,8 @@ def test_state_roundtrip_and_lockstep_rule(venv, flib):
     assert ep.info()["steps_since_reset"] == -1
 
 
-def test_metrics_and_partials(venv):
-    F, N = 500, 5
+@pytest.mark.parametrize("F,N", [(500, 5), (4, 1500)])
+def test_metrics_and_partials(venv, F, N):
     env = make_env(venv, F, N, True, 21, max_steps=3)
     ref = COracleEnv(F, N, True, 21, max_steps=3)
     env.reset()
@@ -298,7 +300,8 @@ def test_metrics_and_partials(venv):
 
 
 @pytest.mark.parametrize("N,mode", [(5, "mt19937"), (10, "philox"), (1, "mt19937"),
-                                    (64, "philox"), (100, "mt19937")])
+                                    (64, "philox"), (100, "mt19937"), (1500, "philox"),
+                                    (2049, "mt19937")])
 def test_reward_components_every_step_incl_done(venv, N, mode):
     """fenv_metrics columns 4-7: the means of compute_reward_and_done's logged components
     (simulate.py:183-208) of the state each step scored -- on a done step the terminal
@@ -489,7 +492,10 @@ def test_visualize_mirror(venv):
                                                 (7, "mt19937", 25, 2, 40),
                                                 # >= 2048 waves: the workgroup-staged kernel
                                                 (5, "mt19937", 12, 4, 30001),
-                                                (10, "philox", 10, 1, 13000)])
+                                                (10, "philox", 10, 1, 13000),
+                                                # large formations (k_rollout_large)
+                                                (1500, "philox", 7, 3, 40),
+                                                (1100, "mt19937", 13, 5, 40)])
 def test_rollout_random_actions(venv, N, mode, T, offset, F):
     """fenv_rollout_random: the in-kernel actions are oracle.philox_actions bit for bit (also
     for a shard), and the rollout equals fenv_rollout fed with those actions from the same state
@@ -560,7 +566,8 @@ def test_empty_launches_are_no_ops(venv, mode):
         make_env(venv, 0, N)
 
 
-@pytest.mark.parametrize("F,N,T", [(4096, 5, 10), (65536, 10, 10), (300, 64, 3), (2000, 5, 1)])
+@pytest.mark.parametrize("F,N,T", [(4096, 5, 10), (65536, 10, 10), (300, 64, 3), (2000, 5, 1),
+                                   (5, 1500, 4)])
 def test_null_outputs_take_general_kernels_same_results(venv, flib, F, N, T):
     """fenv_rollout with obs or rew/done passed as NULL through the C ABI skips those stores
     only: the state it leaves and the rows it does write equal the all-outputs launch's, at the

@@ -57,8 +57,8 @@ def test_gae_kernel(mods):
     np.testing.assert_allclose(buf.returns.cpu().numpy(), ret, rtol=1e-5, atol=1e-5)
 
 
-def test_collect_matches_stepwise(mods):
-    F, N = 300, 5
+@pytest.mark.parametrize("F,N", [(300, 5), (2, 1500)])  # fused kernel / unfused (N > 64)
+def test_collect_matches_stepwise(mods, F, N):
     cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": True}
     env1 = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=3)
     env2 = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=3)
