@@ -222,6 +222,13 @@ def policy_rollout_roofline(kernel_ms: float):
         out["mfma_busy_frac"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (kernel_ms * 1e-3) / peak
     if "SQ_WAVE_CYCLES" in k:
         out["avg_waves_per_simd"] = 4.0 * k["SQ_WAVE_CYCLES"] / (kernel_ms * 1e-3) / peak
+    if "GRBM_GUI_ACTIVE" in k and "SQ_ACTIVE_INST_ANY" in k:
+        # within the profiled run itself: the share of the clocked SIMD-cycles (GRBM_GUI_ACTIVE is
+        # summed over the 8 XCDs) in which the SIMD issued any instruction (VALU, MFMA, LDS,
+        # SALU, branch) -- how close the kernel is to the issue limit, whatever the clock
+        clocked = k["GRBM_GUI_ACTIVE"] / 8.0 * SIMDS
+        out["issue_busy_frac_clocked"] = 4.0 * k["SQ_ACTIVE_INST_ANY"] / clocked
+        out["valu_busy_frac_clocked"] = 4.0 * k["SQ_ACTIVE_INST_VALU"] / clocked
     return out
 
 
