@@ -402,7 +402,8 @@ def hbm_ceiling(acts, obs, rew, done, A: int, T: int, D: int, stream, reps: int 
     return {"achieved": byts / (ms * 1e-3) / 1e9, "unit": "GB/s", "ms_per_launch": ms,
             "agents": Ac, "steps": T,
             "kernel": "k_mix (tools/calib/hbm_ceiling.hip): the launch's action read and obs / "
-                      "reward / done writes, no arithmetic, whole aligned float4 runs"}
+                      "reward / done writes, no arithmetic, whole aligned float4 runs; the "
+                      "faster of plain and non-temporal stores"}
 
 
 def launch_plan(steps: int, T: int) -> list[int]:

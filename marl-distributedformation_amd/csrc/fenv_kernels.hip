@@ -74,6 +74,7 @@ struct RSStage {
 // rows [kfirst, kfirst + nrows) of the slice from the LDS buffers (all kRSA threads).  Vector
 // path: thread (c4 = tid & 127, tid >> 7) stores 16 B of reward / 4 B of done per row, 4 rows per
 // pass (a slice has at most kRSA = 512 agents = 128 float4).
+template <bool NT>
 __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows, int64_t A,
                                          float *__restrict__ rew, uint8_t *__restrict__ done) {
     const int tid = threadIdx.x, n = r.nwg;
@@ -84,8 +85,8 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
         if (vec && (reinterpret_cast<uintptr_t>(base) & 15) == 0) {
             if (c4 < (n >> 2))
                 for (int row = r0; row < nrows; row += 4)
-                    reinterpret_cast<float4 *>(base + (int64_t)row * A)[c4] =
-                        reinterpret_cast<const float4 *>(r.rbuf + row * kRSA)[c4];
+                    st_out<NT>(reinterpret_cast<float4 *>(base + (int64_t)row * A) + c4,
+                           reinterpret_cast<const float4 *>(r.rbuf + row * kRSA)[c4]);
         } else if (tid < n) {
             for (int row = 0; row < nrows; ++row)
                 base[(int64_t)row * A + tid] = r.rbuf[row * kRSA + tid];
@@ -96,8 +97,8 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
         if (vec && (reinterpret_cast<uintptr_t>(base) & 3) == 0) {
             if (c4 < (n >> 2))
                 for (int row = r0; row < nrows; row += 4)
-                    reinterpret_cast<uint32_t *>(base + (int64_t)row * A)[c4] =
-                        reinterpret_cast<const uint32_t *>(r.dbuf + row * kRSA)[c4];
+                    st_out<NT>(reinterpret_cast<uint32_t *>(base + (int64_t)row * A) + c4,
+                           reinterpret_cast<const uint32_t *>(r.dbuf + row * kRSA)[c4]);
         } else if (tid < n) {
             for (int row = 0; row < nrows; ++row)
                 base[(int64_t)row * A + tid] = r.dbuf[row * kRSA + tid];
@@ -111,7 +112,7 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
 // reward / done / the stats sums / the terminal and final state, kRoleObs only the observations.
 constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2;
 
-template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll>
+template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll, bool NT = false>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
@@ -170,15 +171,15 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         float o[8];
         env_obs<D>(x, s, o);
         if (ROLE != kRoleState && obs)
-            store_obs_rows<D>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
+            store_obs_rows<D, NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
         if (ROLE != kRoleObs && active) {
             if (RS) {
                 const int kb = k % kRSTB;
                 rsg.rbuf[kb * kRSA + rsg.li] = rw;
                 rsg.dbuf[kb * kRSA + rsg.li] = (uint8_t)dn;
             } else {
-                if (rew) rew[row] = rw;
-                if (done) done[row] = (uint8_t)dn;
+                if (rew) st_out<NT>(rew + row, rw);
+                if (done) st_out<NT>(done + row, (uint8_t)dn);
             }
             rsum += rw;
             dsum += dn ? 1.0f : 0.0f;
@@ -191,7 +192,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
 #pragma unroll 1
             for (int32_t k = kc; k < ke; ++k) step(k, 0);
             __syncthreads();
-            rs_flush(rsg, kc, ke - kc, A, rew, done);
+            rs_flush<NT>(rsg, kc, ke - kc, A, rew, done);
             if (ke < T) __syncthreads();
         }
     } else {
@@ -218,7 +219,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
     }
 }
 
-template <int D, int MODE, bool RA, int PF>
+template <int D, int MODE, bool RA, int PF, bool NT>
 __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, DevPending p,
                                                       int32_t T, const float2 *__restrict__ act,
                                                       ActGen gen,
@@ -245,7 +246,8 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
     const int M = (int)((f_left <= 0 ? 0 : (f_left < c.fpw ? f_left : c.fpw)) * N);
     float rsum = 0.f, dsum = 0.f;
     if (M > 0)
-        rollout_body<D, MODE, RA, false, PF>(c, st, p, x, active, f, a, i, stage[w], lane, M,
+        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleAll, NT>(c, st, p, x, active, f, a, i,
+                                                                  stage[w], lane, M,
                                              f_first * N, T, act, gen, obs, rew, done, rsum,
                                              dsum);
     if (partial) {  // one {sum reward, sum done} record per workgroup, fixed summation order
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState s
     }
 }
 
-template <int D, int MODE, bool RA>
+template <int D, int MODE, bool RA, bool NT>
 __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, DevState st, DevPending p,
                                                           int32_t T,
                                                           const float2 *__restrict__ act,
@@ -360,7 +362,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     rsg.g0 = blk * kRS * Mw;
     rsg.nwg = (int)((A - rsg.g0) < (int64_t)kRS * Mw ? (A - rsg.g0) : (int64_t)kRS * Mw);
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA, true, 1>(c, st, p, x, active, f, a, i, stage[w], lane, M,
+    rollout_body<D, MODE, RA, true, 1, WaveX, kRoleAll, NT>(c, st, p, x, active, f, a, i, stage[w],
+                                                           lane, M,
                                        f_first * N, T, act, gen, obs, rew, done, rsum, dsum, rsg);
     if (partial) {  // one {sum reward, sum done} record per 4 waves -- the same records, in the
                     // same summation order, as k_rollout_wave's 4-wave workgroups
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     }
 }
 
-template <int D, int MODE, bool RA>
+template <int D, int MODE, bool RA, bool NT>
 __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, DevPending p,
                                                         int32_t T,
                                                         const float2 *__restrict__ act,
@@ -403,7 +406,8 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     const int w = i >> 6;
     const int M = N - 64 * w < 64 ? (N - 64 * w > 0 ? N - 64 * w : 0) : 64;
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA, false, 1>(c, st, p, x, active, f, a, i, stage[w], i & 63, M,
+    rollout_body<D, MODE, RA, false, 1, BlockX, kRoleAll, NT>(c, st, p, x, active, f, a, i,
+                                                             stage[w], i & 63, M,
                                         f * N + 64 * w, T, act, gen, obs, rew, done, rsum, dsum);
     if (partial) {
         rsum = wave_sum(rsum);
@@ -733,22 +737,22 @@ static inline int64_t rs_blocks(const Consts &c) {
 
 static inline unsigned block_threads(int32_t N) { return (unsigned)((N + 63) / 64 * 64); }
 
-template <int D, int MODE>
-static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
+template <int D, int MODE, bool NT>
+static hipError_t rollout_dmn(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                              const float *act, float *obs, float *rew, uint8_t *done,
                              float *partial, bool accum, hipStream_t st, const ActGen *gen) {
     const float2 *a2 = reinterpret_cast<const float2 *>(act);
     float2 *p2 = reinterpret_cast<float2 *>(partial);
     if (gen) {  // in-kernel actions
         if (use_rs(c, T))
-            hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, true>),
+            hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, true, NT>),
                                dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p,
                                T, a2, *gen, obs, rew, done, p2, accum);
         else if (wave_path(c.N))
-            hipLaunchKernelGGL((k_rollout_wave<D, MODE, true, 1>), dim3((unsigned)group_count(c)),
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, true, 1, NT>), dim3((unsigned)group_count(c)),
                                dim3(256), 0, st, c, s, p, T, a2, *gen, obs, rew, done, p2, accum);
         else
-            hipLaunchKernelGGL((k_rollout_block<D, MODE, true>), dim3((unsigned)c.F),
+            hipLaunchKernelGGL((k_rollout_block<D, MODE, true, NT>), dim3((unsigned)c.F),
                                dim3(block_threads(c.N)), 0, st, c, s, p, T, a2, *gen, obs, rew,
                                done, p2, accum);
         return hipGetLastError();
@@ -763,7 +767,7 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
     }
 #endif
     if (use_rs(c, T)) {
-        hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false>),
+        hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false, NT>),
                            dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
                            a2, g0, obs, rew, done, p2, accum);
     } else if (use_split(c)) {
@@ -777,17 +781,40 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
     } else if (wave_path(c.N)) {
         const unsigned blocks = (unsigned)group_count(c);
         if (use_pf(c, T))
-            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, FENV_SMALL_PF>), dim3(blocks),
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, FENV_SMALL_PF, NT>), dim3(blocks),
                                dim3(256), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
         else
-            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, 1>), dim3(blocks), dim3(256), 0, st,
+            hipLaunchKernelGGL((k_rollout_wave<D, MODE, false, 1, NT>), dim3(blocks), dim3(256), 0, st,
                                c, s, p, T, a2, g0, obs, rew, done, p2, accum);
     } else {
-        hipLaunchKernelGGL((k_rollout_block<D, MODE, false>), dim3((unsigned)c.F),
+        hipLaunchKernelGGL((k_rollout_block<D, MODE, false, NT>), dim3((unsigned)c.F),
                            dim3(block_threads(c.N)), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2,
                            accum);
     }
     return hipGetLastError();
+}
+
+// Non-temporal output stores (st_out) where a launch's outputs stream far past the caches: at
+// least kNTMinAgentSteps agent-steps (45 B each at D = 8: >= 135 MB, half the Infinity Cache).
+// Same-box A/B (profiles/ab/r2_nt_out_ab.txt): config 3 447 vs 470 us per 10-step launch,
+// config 4 74-75 vs 94 us, single-step launches at config 3 52 vs 70 us; config 1 (200k
+// agent-steps, latency-bound) 8.2 vs 7.7 us, so small launches keep plain stores.
+#ifndef FENV_NT_OUT
+#define FENV_NT_OUT 1
+#endif
+constexpr double kNTMinAgentSteps = 3.0e6;
+static inline bool use_nt(const Consts &c, int32_t T) {
+    return FENV_NT_OUT && (double)c.F * (double)c.N * (double)T >= kNTMinAgentSteps;
+}
+
+template <int D, int MODE>
+static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
+                             const float *act, float *obs, float *rew, uint8_t *done,
+                             float *partial, bool accum, hipStream_t st, const ActGen *gen) {
+    return use_nt(c, T) ? rollout_dmn<D, MODE, true>(c, s, p, T, act, obs, rew, done, partial,
+                                                     accum, st, gen)
+                        : rollout_dmn<D, MODE, false>(c, s, p, T, act, obs, rew, done, partial,
+                                                      accum, st, gen);
 }
 
 const char *rollout_kernel_name(const Consts &c, int32_t T) {

@@ -18,4 +18,6 @@ out = []
 for name, F, N, launches in (("c1", 4096, 5, 1000), ("c4", 16384, 64, 100), ("c3", 1 << 20, 5, 100)):
     r = bench.env_config_bench(pkg.__name__, dev, F, N, launches)
     out.append(f"{name} {r['avg_kernel_ms'] * 1e3:7.2f} us")
+r = bench.env_config_bench(pkg.__name__, dev, 1 << 20, 5, 100, T=1)  # the fenv_step face
+out.append(f"c3/T1 {r['avg_kernel_ms'] * 1e3:6.2f} us")
 print(f"{lib:36s} " + "  ".join(out), flush=True)
