@@ -597,3 +597,29 @@ def test_null_outputs_take_general_kernels_same_results(venv, flib, F, N, T):
     for sa, sb, sc in zip(full[3], no_obs[3], no_rew[3]):
         assert torch.equal(sa, sb) and torch.equal(sa, sc)
     assert not (full[0] == -7.0).any() and not (full[1] == -7.0).any()
+
+
+def test_randomized_shapes_vs_oracle(venv):
+    """Property test over the env's configuration space (hypothesis, derandomized so every run
+    checks the same 60 cases): formation sizes across the wavefront / workgroup / large-formation
+    paths, both observation layouts, launch lengths that straddle MT19937 reset events (short
+    episodes), in-range, out-of-bounds-heavy and extreme actions -- bit for bit against the C
+    oracle over every step and the final state."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    sizes = st.one_of(st.integers(1, 70), st.sampled_from([96, 127, 200, 513, 1024, 1025, 1300]))
+
+    @settings(max_examples=60, deadline=None, derandomize=True, database=None,
+              suppress_health_check=list(HealthCheck))
+    @given(N=sizes, fa=st.integers(1, 4000), goal=st.booleans(), steps=st.integers(1, 30),
+           chunks=st.lists(st.integers(1, 12), min_size=1, max_size=3),
+           amp=st.sampled_from([0.5, 1.2, 40.0, -1.0]), max_steps=st.integers(0, 12),
+           seed=st.integers(0, 2**32 - 1))
+    def check(N, fa, goal, steps, chunks, amp, max_steps, seed):
+        F = max(1, min(fa, 20000 // N))
+        with np.errstate(over="ignore", invalid="ignore"):
+            run_vs_oracle(venv, F, N, goal, seed, steps=steps, chunks=chunks, amp=amp,
+                          max_steps=max_steps)
+
+    check()
