@@ -37,7 +37,7 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
 #ifndef FENV_RS_TB
 #define FENV_RS_TB 8
 #endif
-// Register budget: left to the compiler (79 VGPRs -> 6 waves/SIMD, 3 workgroups per CU).  Forcing
+// Register budget: left to the compiler (75 VGPRs -> 6 waves/SIMD, 3 workgroups per CU).  Forcing
 // 64 VGPRs (4 workgroups per CU) spills and runs ~12 % slower (tools/env_ab.sh).
 #ifndef FENV_RS_OCC
 #define FENV_RS_OCC
