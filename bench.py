@@ -356,8 +356,8 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
             "ms_per_update": el / updates * 1e3, "us_per_minibatch": per_mb * 1e6,
             "samples_per_s": n * m.cfg.n_epochs / (el / updates),
             "gflops": flop / per_mb / 1e9,
-            "note": "one workgroup (a minibatch depends on the previous one's parameters); "
-                    "single-CU fp32 peak is ~614 GFLOP/s"}
+            "note": "actor and critic on one CU each (a minibatch depends on the previous "
+                    "one's parameters); one CU's fp32 peak is ~614 GFLOP/s"}
 
 
 def load_pmc_traffic(workload: str):

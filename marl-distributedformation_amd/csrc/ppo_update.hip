@@ -6,9 +6,12 @@
 // loss + ent_coef * entropy loss, backward, clip_grad_norm_(0.5), Adam(eps 1e-5).  The torch
 // restatement of the same update is ppo.py (graph / eager paths); this kernel is its fused form.
 //
-// Why one workgroup: a minibatch step depends on the previous step's parameters, and a 64-sample
-// step of this 9,669-parameter MLP is ~1.8 MFLOP -- far too little to spread over the chip, and
-// ~100 tiny launches per step in torch (~430 us replayed as a HIP graph).  Here the parameters,
+// Why one workgroup per network: a minibatch step depends on the previous step's parameters,
+// and a 64-sample step of this 9,669-parameter MLP is ~1.8 MFLOP -- far too little to spread
+// over the chip, and ~100 tiny launches per step in torch (~430 us replayed as a HIP graph).
+// The actor and the critic only couple through the global gradient norm, so by default they run
+// as two workgroups on two CUs (FENV_PPO_SPLIT below); FENV_PPO_SPLIT=0 is the one-workgroup
+// form of the same code.  Here the parameters,
 // their gradients and the minibatch's activations live in LDS (152 KB), each thread keeps the
 // Adam moments of the ~19 parameters it owns in registers, and the loop runs every minibatch of
 // every epoch inside one launch.  The 64-deep contractions (layer 2 forward, W2 gradients,
@@ -82,7 +85,19 @@ struct PPOArgs {
     int32_t D, n_epochs, batch_size;
     ppo_hparams hp;
     double *stats;
+    uint64_t *xch;  // split launch: the two blocks' {minibatch + 1, partial grad norm^2} words
 };
+
+// Split launch (FENV_PPO_SPLIT): the actor and the critic each on their own CU.  The two networks'
+// forward, loss and backward are independent; the only coupling is clip_grad_norm_'s global norm,
+// exchanged once per minibatch through two 64-bit words in L2 (the working blocks are 0 and 8,
+// which the dispatcher places on the same XCD).  Each block runs the unsplit kernel's four waves
+// of its network on one CU, one wave per SIMD, and updates only its own parameters.
+#ifndef FENV_PPO_SPLIT
+#define FENV_PPO_SPLIT 1
+#endif
+constexpr int kPTS = 256;   // threads per block, split launch
+constexpr int kPerTS = 20;  // parameters owned per thread, split launch (actor: 4,868 at D = 8)
 
 // tanh x = 1 - 2 / (1 + e^(2x)) on v_exp_f32 + v_rcp_f32 (absolute error < 3e-7 over the whole
 // range, +-1 at +-inf) instead of the ~30-instruction libm tanhf: the update's forward only has
@@ -163,30 +178,64 @@ __device__ __forceinline__ float wsum(float v) {
 #define FENV_PPO_PHASE(i)
 #endif
 
-__global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
+template <bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
+    constexpr int NT = SPLIT ? kPTS : kPT;     // threads of a working block
+    constexpr int KP = SPLIT ? kPerTS : kPerT;  // Adam slots per thread
+    if (SPLIT && (blockIdx.x & 7) != 0) return;  // split: blocks 0 and 8 work (one XCD)
+    const int net_b = SPLIT ? (int)(blockIdx.x >> 3) : 0;  // split: this block's network
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *W = sm + oPW, *G = sm + oPG, *O = sm + oPO, *H1 = sm + oPH1, *H2 = sm + oPH2;
     float *S = sm + oPS, *R = sm + oPR;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wl = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave of this block
+    const int w = wl + (SPLIT ? 4 * net_b : 0);               // wave index of the unsplit kernel
     const int D = g.D;
     const PLayout L(D);
     const int P = L.total;
     const ppo_hparams hp = g.hp;
+    // parameter of Adam slot q of this thread (P: none).  Split: the block's network only --
+    // actor = pi* layers, action head, log_std; critic = vf* layers, value head.
+    auto own = [&](int q) -> int {
+        int i = tid + q * NT;
+        if (!SPLIT) return i < P ? i : P;
+        if (net_b == 0) {
+            const int n0 = L.vf0W - L.pi0W, n1 = L.valW - L.actW;
+            if (i < n0) return L.pi0W + i;
+            i -= n0;
+            if (i < n1) return L.actW + i;
+            i -= n1;
+            return i < 2 ? L.logstd + i : P;
+        }
+        const int n0 = L.actW - L.vf0W, n1 = L.logstd - L.valW;
+        if (i < n0) return L.vf0W + i;
+        i -= n0;
+        return i < n1 ? L.valW + i : P;
+    };
 
-    for (int p = tid; p < P; p += kPT) W[lx(p)] = g.params[p];
+    for (int p = tid; p < P; p += NT) W[lx(p)] = g.params[p];
     // activations and observations start finite: the MFMA contractions run over all 64 rows
     // and a partial minibatch's unused rows (multiplied by zeros) must not hold NaN bit patterns
-    for (int q = tid; q < 4 * kPB * kRow; q += kPT) H1[q] = 0.0f;  // H1 and H2 are contiguous
-    for (int q = tid; q < kPB * 9; q += kPT) O[q] = 0.0f;
-    float m[kPerT], v[kPerT];  // Adam moments of the parameters this thread owns
+    for (int q = tid; q < 4 * kPB * kRow; q += NT) H1[q] = 0.0f;  // H1 and H2 are contiguous
+    for (int q = tid; q < kPB * 9; q += NT) O[q] = 0.0f;
+    float m[KP], v[KP];  // Adam moments of the parameters this thread owns
 #pragma unroll
-    for (int q = 0; q < kPerT; ++q) {
-        const int p = tid + q * kPT;
+    for (int q = 0; q < KP; ++q) {
+        const int p = own(q);
         m[q] = p < P ? g.exp_avg[p] : 0.0f;
         v[q] = p < P ? g.exp_avg_sq[p] : 0.0f;
     }
     float step = g.step[0];
+    // split: the LDS index of each Adam slot's parameter (-1: none), fixed for the launch
+    int lp[SPLIT ? KP : 1];
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+            const int p = own(q);
+            lp[q] = p < P ? lx(p) : -1;
+        }
+    }
+    bool partner_lost = false;  // split launch: the other block's norm exchange timed out
     const float lb1 = log2f(hp.beta1), lb2 = log2f(hp.beta2);
     double st_pl = 0.0, st_vl = 0.0, st_el = 0.0, st_cf = 0.0;
 #if FENV_PPO_PROFILE
@@ -197,25 +246,31 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 
     const int64_t n = g.n;
     const int bs = g.batch_size;
-    // Gather pipeline (B * 8 <= kPT: a thread moves at most one observation value and, for
+    // Gather pipeline (a thread moves OPT observation values -- B * 8 <= OPT * NT -- and, for
     // tid < B, one sample's act / old_log_prob / adv / ret).  The minibatch's values were loaded
     // into registers during the previous minibatch, from perm indices loaded one minibatch
     // before that, so no gather waits on a dependent global load (the loop's barriers wait on
     // LDS only).  Minibatch k = (epoch, start) in the loop's order; kMB = minibatches per epoch.
     const int64_t kMB = (n + bs - 1) / bs;
     const int64_t nmb = kMB * (int64_t)g.n_epochs;
-    auto perm_rows = [&](int64_t k, int64_t &ro, int64_t &rs) {  // rows this thread gathers
-        ro = rs = -1;
+    constexpr int OPT = (kPB * 8 + NT - 1) / NT;
+    auto perm_rows = [&](int64_t k, int64_t (&ro)[OPT], int64_t &rs) {  // rows this thread gathers
+        rs = -1;
+#pragma unroll
+        for (int j = 0; j < OPT; ++j) ro[j] = -1;
         if (k >= nmb) return;
         const int64_t e = k / kMB, s0k = (k - e * kMB) * bs;
         const int Bk = (int)((n - s0k) < bs ? (n - s0k) : bs);
         const int64_t *pp = g.perm + e * n + s0k;
-        if (tid < Bk * 8) ro = pp[tid >> 3];
+#pragma unroll
+        for (int j = 0; j < OPT; ++j)
+            if (tid + j * NT < Bk * 8) ro[j] = pp[(tid + j * NT) >> 3];
         if (tid < Bk) rs = pp[tid];
     };
-    auto load_rows = [&](int64_t ro, int64_t rs, float &po, float (&ps)[5]) {
-        const int i = tid & 7;
-        po = (ro >= 0 && i < D) ? g.obs[ro * D + i] : 0.0f;
+    auto load_rows = [&](const int64_t (&ro)[OPT], int64_t rs, float (&po)[OPT], float (&ps)[5]) {
+        const int i = tid & 7;  // NT is a multiple of 8: every slot j of a thread has column i
+#pragma unroll
+        for (int j = 0; j < OPT; ++j) po[j] = (ro[j] >= 0 && i < D) ? g.obs[ro[j] * D + i] : 0.0f;
         if (rs >= 0) {
             ps[0] = g.act[2 * rs];
             ps[1] = g.act[2 * rs + 1];
@@ -224,10 +279,10 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             ps[4] = g.ret[rs];
         }
     };
-    float po = 0.0f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    int64_t ro_n, rs_n;  // perm rows of the next minibatch
+    float po[OPT], ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    int64_t ro_n[OPT], rs_n;  // perm rows of the next minibatch
     {
-        int64_t ro0, rs0;
+        int64_t ro0[OPT], rs0;
         perm_rows(0, ro0, rs0);
         load_rows(ro0, rs0, po, ps);
         perm_rows(1, ro_n, rs_n);
@@ -239,7 +294,11 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             const float invB = 1.0f / (float)B;
             float gss = 0.f;  // sum of squares of the gradient entries this thread writes
             // ---- gather the minibatch (from the prefetch registers), then start the next one
-            if (tid < B * 8) O[(tid >> 3) * 9 + (tid & 7)] = po;
+#pragma unroll
+            for (int j = 0; j < OPT; ++j) {
+                const int e = tid + j * NT;
+                if (e < B * 8) O[(e >> 3) * 9 + (e & 7)] = po[j];
+            }
             if (tid < B) {
                 S[sA0 * kPB + tid] = ps[0];
                 S[sA1 * kPB + tid] = ps[1];
@@ -345,8 +404,11 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(2);
-            // ---- heads, losses and per-sample gradients (wave 0, lane = sample)
-            if (w == 0) {
+            // ---- heads, losses and per-sample gradients (wave 0, lane = sample; split: wave 0 of
+            // each block, the actor block keeping the policy/entropy terms, the critic block the
+            // value terms)
+            if (wl == 0) {
+                const bool do_pi = !SPLIT || net_b == 0, do_vf = !SPLIT || net_b == 1;
                 const bool on = lane < B;
                 const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
                 const float sd0 = expf(ls0), sd1 = expf(ls1);
@@ -383,9 +445,11 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     gls0 = dlp * (d0 * d0 / var0 - 1.0f);
                     gls1 = dlp * (d1 * d1 / var1 - 1.0f);
                 }
-                S[sGMU0 * kPB + lane] = gmu0;
-                S[sGMU1 * kPB + lane] = gmu1;
-                S[sGV * kPB + lane] = gv;
+                if (do_pi) {
+                    S[sGMU0 * kPB + lane] = gmu0;
+                    S[sGMU1 * kPB + lane] = gmu1;
+                }
+                if (do_vf) S[sGV * kPB + lane] = gv;
                 pl = wsum(pl);
                 vl = wsum(vl);
                 cf = wsum(cf);
@@ -393,20 +457,27 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                 gls1 = wsum(gls1);
                 const float sgmu0 = wsum(gmu0), sgmu1 = wsum(gmu1), sgv = wsum(gv);
                 if (lane == 0) {
-                    const float kHalfLog2PiE = 1.41893853320467274f;  // 0.5 + 0.5 log(2 pi)
-                    const float ent = (kHalfLog2PiE + lsd0) + (kHalfLog2PiE + lsd1);
-                    st_pl += (double)(-pl * invB);
-                    st_vl += (double)(vl * invB);
-                    st_el += (double)(-ent);
-                    st_cf += (double)(cf * invB);
-                    // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls = 1)
-                    const float g0 = gls0 - hp.ent_coef, g1 = gls1 - hp.ent_coef;
-                    G[lx(L.logstd)] = g0;
-                    G[lx(L.logstd + 1)] = g1;
-                    G[lx(L.actb)] = sgmu0;
-                    G[lx(L.actb + 1)] = sgmu1;
-                    G[lx(L.valb)] = sgv;
-                    gss = g0 * g0 + g1 * g1 + sgmu0 * sgmu0 + sgmu1 * sgmu1 + sgv * sgv;
+                    gss = 0.0f;
+                    if (do_pi) {
+                        const float kHalfLog2PiE = 1.41893853320467274f;  // 0.5 + 0.5 log(2 pi)
+                        const float ent = (kHalfLog2PiE + lsd0) + (kHalfLog2PiE + lsd1);
+                        st_pl += (double)(-pl * invB);
+                        st_el += (double)(-ent);
+                        st_cf += (double)(cf * invB);
+                        // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls
+                        // = 1)
+                        const float g0 = gls0 - hp.ent_coef, g1 = gls1 - hp.ent_coef;
+                        G[lx(L.logstd)] = g0;
+                        G[lx(L.logstd + 1)] = g1;
+                        G[lx(L.actb)] = sgmu0;
+                        G[lx(L.actb + 1)] = sgmu1;
+                        gss = g0 * g0 + g1 * g1 + sgmu0 * sgmu0 + sgmu1 * sgmu1;
+                    }
+                    if (do_vf) {
+                        st_vl += (double)(vl * invB);
+                        G[lx(L.valb)] = sgv;
+                        gss += sgv * sgv;
+                    }
                 }
             }
             __syncthreads();
@@ -516,8 +587,8 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     Gr[rho(r, h) * kRow] = gw[r];
                     gss = __builtin_fmaf(gw[r], gw[r], gss);
                 }
-                if (tid < 2 * kHid) {
-                    const int bn = tid >> 6, j = tid & 63;
+                if (tid < (SPLIT ? kHid : 2 * kHid)) {
+                    const int bn = SPLIT ? net_b : tid >> 6, j = tid & 63;
                     const float *z2 = H2 + bn * kPB * kRow + j;
                     const float acc = col_sum(z2, B);
                     G[lx((bn ? L.vf2b : L.pi2b) + j)] = acc;
@@ -557,8 +628,8 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
                     }
                 }
             }
-            if (tid < 2 * kHid) {
-                const int net = tid >> 6, j = tid & 63;
+            if (tid < (SPLIT ? kHid : 2 * kHid)) {
+                const int net = SPLIT ? net_b : tid >> 6, j = tid & 63;
                 const float *z1 = H1 + net * kPB * kRow + j;
                 const float acc = col_sum(z1, B);
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
@@ -568,12 +639,50 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             // accumulated as it wrote its gradient entries (every entry is written exactly once
             // per minibatch), one wave sum each, reduced after the barrier
             gss = wsum(gss);
-            if (lane == 0) R[w] = gss;
+            if (lane == 0) R[wl] = gss;
             __syncthreads();
             FENV_PPO_PHASE(8);
-            FENV_PPO_PHASE(9);
+            // split: this thread's gradient and parameter entries are read now, so the LDS
+            // reads overlap the norm exchange below
+            float gq[SPLIT ? KP : 1], wq[SPLIT ? KP : 1];
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int q = 0; q < KP; ++q) {
+                    gq[q] = lp[q] >= 0 ? G[lp[q]] : 0.0f;
+                    wq[q] = lp[q] >= 0 ? W[lp[q]] : 0.0f;
+                }
+            }
             float tot = 0.f;
-            for (int q = 0; q < kPT / 64; ++q) tot += R[q];
+            for (int q = 0; q < NT / 64; ++q) tot += R[q];
+            if (SPLIT) {
+                // the other network's partial (actor's first in the sum on both blocks).  The
+                // wait is bounded: a missing partner poisons the update with NaN instead of
+                // hanging the GPU.
+                if (tid == 0) {
+                    const uint64_t seq = (uint64_t)(kmb + 1);
+                    // one 64-bit word carries both the value and its sequence number, so relaxed
+                    // device-scope atomics suffice (nothing else is published through it)
+                    __hip_atomic_store(g.xch + net_b, (seq << 32) | __float_as_uint(tot),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint64_t o = 0;
+                    // after one timed-out wait the partner is taken as lost for good: no further
+                    // waits, so a broken launch ends in milliseconds, not one timeout per
+                    // minibatch
+                    const int max_spin = partner_lost ? 0 : (1 << 22);
+                    for (int spin = 0; spin < max_spin; ++spin) {
+                        o = __hip_atomic_load(g.xch + (net_b ^ 1), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                        if ((o >> 32) == seq) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    partner_lost = (o >> 32) != seq;
+                    const float other = partner_lost ? __builtin_nanf("") : __uint_as_float((uint32_t)o);
+                    R[32] = net_b == 0 ? tot + other : other + tot;
+                }
+                __syncthreads();
+                tot = R[32];
+            }
+            FENV_PPO_PHASE(9);
             const float norm = __builtin_sqrtf(tot);
             float coef = hp.max_grad_norm / (norm + 1e-6f);
             coef = coef < 1.0f ? coef : 1.0f;
@@ -584,26 +693,31 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
             const float step_size = hp.lr / bc1;
             const float inv_bc2s = 1.0f / __builtin_sqrtf(bc2);
 #pragma unroll
-            for (int q = 0; q < kPerT; ++q) {
-                const int p = tid + q * kPT;
+            for (int q = 0; q < KP; ++q) {
+                const int p = SPLIT ? (lp[q] >= 0 ? 0 : P) : own(q);
                 if (p < P) {
-                    const float gr = G[lx(p)] * coef;
+                    const int ix = SPLIT ? lp[q] : lx(p);
+                    const float gr = (SPLIT ? gq[q] : G[ix]) * coef;
                     m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
                     v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
                     // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
                     // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
                     const float den = __builtin_amdgcn_sqrtf(v[q]) * inv_bc2s + hp.eps;
-                    W[lx(p)] = W[lx(p)] - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
+                    W[ix] = (SPLIT ? wq[q] : W[ix]) - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
                 }
             }
             __syncthreads();
             FENV_PPO_PHASE(10);
         }
     }
-    for (int p = tid; p < P; p += kPT) g.params[p] = W[lx(p)];
 #pragma unroll
-    for (int q = 0; q < kPerT; ++q) {
-        const int p = tid + q * kPT;
+    for (int q = 0; q < KP; ++q) {
+        const int p = own(q);
+        if (p < P) g.params[p] = W[lx(p)];
+    }
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        const int p = own(q);
         if (p < P) {
 #if FENV_PPO_DUMP_GRAD  // diagnostic build: the last minibatch's unclipped gradient, its
                         // observations and dL/dz1 rows
@@ -616,16 +730,20 @@ __global__ __launch_bounds__(kPT) void k_ppo_update(PPOArgs g) {
 #endif
         }
     }
-    if (tid == 0) {
+    if (tid == 0 && net_b == 0) {
         g.step[0] = step;
         g.stats[0] += st_pl;
-        g.stats[1] += st_vl;
+        if (!SPLIT) g.stats[1] += st_vl;
         g.stats[2] += st_el;
         g.stats[3] += st_cf;
 #if FENV_PPO_PROFILE
         for (int q = 0; q < 11; ++q) g.stats[4 + q] += prof[q];
 #endif
     }
+    if (SPLIT && tid == 0 && net_b == 1) g.stats[1] += st_vl;
+    // split: a norm exchange that timed out leaves NaN parameters; say so in the policy-loss
+    // slot too, which the host checks (ppo.py raises)
+    if (SPLIT && tid == 0 && partner_lost) g.stats[0] = __builtin_nan("");
 }
 
 hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
@@ -634,17 +752,42 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
                              int64_t n, const int64_t *perm, int32_t n_epochs,
                              int32_t batch_size, const ppo_hparams &hp, double *stats,
                              hipStream_t st) {
+    constexpr bool split = FENV_PPO_SPLIT != 0;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_ppo_update),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_ppo_update<split>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kPPOLdsBytes);
         if (e != hipSuccess) return e;
         attr = true;
     }
+    uint64_t *xch = nullptr;
+    if (split) {
+        // exchange words, one pair per device, cleared before every launch (sequence numbers
+        // restart at 1)
+        static uint64_t *words[64] = {};
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+        if (!words[dev]) {
+            e = hipMalloc(&words[dev], 2 * sizeof(uint64_t));
+            if (e != hipSuccess) return e;
+        }
+        xch = words[dev];
+        e = hipMemsetAsync(xch, 0, 2 * sizeof(uint64_t), st);
+        if (e != hipSuccess) return e;
+        const PLayout L(D);
+        if ((L.vf0W - L.pi0W) + (L.valW - L.actW) + 2 > kPTS * kPerTS ||
+            (L.actW - L.vf0W) + (L.logstd - L.valW) > kPTS * kPerTS)
+            return hipErrorInvalidValue;
+    }
     PPOArgs g{params, exp_avg, exp_avg_sq, step, obs, act, old_log_prob, adv, ret, perm, n,
-              D, n_epochs, batch_size, hp, stats};
-    hipLaunchKernelGGL(k_ppo_update, dim3(1), dim3(kPT), kPPOLdsBytes, st, g);
+              D, n_epochs, batch_size, hp, stats, xch};
+    if (split)
+        hipLaunchKernelGGL(k_ppo_update<true>, dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
+    else
+        hipLaunchKernelGGL(k_ppo_update<false>, dim3(1), dim3(kPT), kPPOLdsBytes, st, g);
     return hipGetLastError();
 }
 

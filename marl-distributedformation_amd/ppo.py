@@ -272,6 +272,9 @@ class PPO:
             ctypes.byref(hp), _lib.ptr(self._sums), _lib.current_stream(dev)), "ppo_update")
         steps = c.n_epochs * (-(-n // bs))
         m = (self._sums / steps).tolist()
+        if math.isnan(m[0]):
+            raise RuntimeError("fused PPO update: NaN policy loss (the update diverged, or the "
+                               "two-CU launch's gradient-norm exchange timed out)")
         self.stats = dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2],
                           clip_fraction=m[3])
         return self.stats

@@ -618,6 +618,9 @@ def test_randomized_shapes_vs_oracle(venv):
            seed=st.integers(0, 2**32 - 1))
     def check(N, fa, goal, steps, chunks, amp, max_steps, seed):
         F = max(1, min(fa, 20000 // N))
+        if os.environ.get("FENV_TEST_TRACE"):
+            print(f"case F={F} N={N} goal={goal} steps={steps} chunks={chunks} amp={amp} "
+                  f"max_steps={max_steps} seed={seed}", flush=True)
         with np.errstate(over="ignore", invalid="ignore"):
             run_vs_oracle(venv, F, N, goal, seed, steps=steps, chunks=chunks, amp=amp,
                           max_steps=max_steps)
