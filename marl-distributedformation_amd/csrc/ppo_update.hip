@@ -765,7 +765,7 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
     if (split) {
         // exchange words, one pair per device, cleared before every launch (sequence numbers
         // restart at 1)
-        static uint64_t *words[64] = {};
+        static uint64_t *words[64] = {};  // 16 B per device, kept for the process lifetime
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
