@@ -280,8 +280,10 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
         if (rc) return rc;
         e->term_valid = true;
     }
+    const bool nt = fenvk::rollout_nt(e->c, T);
+    const int64_t chunk = fenvk::rollout_launch_steps(e->c, T);
     while (k0 < T) {
-        int64_t L = T - k0;
+        int64_t L = std::min<int64_t>(T - k0, chunk);
         bool event = false;
         if (e->c.reset_mode == FENV_RESET_MT19937) {
             if (e->t_common < 0)
@@ -302,7 +304,7 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
         FENV_HIP(fenvk::launch_rollout(
             e->c, e->s, e->pending(), (int32_t)L, (int32_t)D, act ? act + k0 * A * 2 : nullptr,
             obs ? obs + k0 * A * D : nullptr, rew ? rew + k0 * A : nullptr,
-            done ? done + k0 * A : nullptr, partial, k0 > 0, st, gen ? &g : nullptr));
+            done ? done + k0 * A : nullptr, partial, k0 > 0, nt, st, gen ? &g : nullptr));
         e->advance_t(L);
         if (event) {
             int rc = e->gen_pending(st);

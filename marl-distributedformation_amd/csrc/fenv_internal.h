@@ -63,9 +63,15 @@ struct ActGen {
     float *out;       // optional [T][A][2] copy of the actions (NULL: not written)
 };
 
+// Launch plan of a T-step rollout call (fenv_rollout / fenv_rollout_random / fenv_step): calls
+// of at least kNTMinAgentSteps agent-steps store their outputs non-temporally (rollout_nt) and
+// run as kernel launches of at most rollout_launch_steps() steps each (fenv_api.cpp splits them,
+// as it splits at MT19937 reset events); the state makes the round trip between the launches.
+bool rollout_nt(const Consts &c, int64_t T);
+int32_t rollout_launch_steps(const Consts &c, int64_t T);
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
-                          float *partial, bool accumulate, hipStream_t st,
+                          float *partial, bool accumulate, bool nt, hipStream_t st,
                           const ActGen *gen = nullptr);
 hipError_t launch_reset_observe(const Consts &c, const DevState &s, const DevPending &p,
                                 int32_t D, bool do_reset, float *obs, hipStream_t st);

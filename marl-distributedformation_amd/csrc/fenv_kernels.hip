@@ -794,27 +794,40 @@ static hipError_t rollout_dmn(const Consts &c, const DevState &s, const DevPendi
     return hipGetLastError();
 }
 
-// Non-temporal output stores (st_out) where a launch's outputs stream far past the caches: at
+// Non-temporal output stores (st_out) where a call's outputs stream far past the caches: at
 // least kNTMinAgentSteps agent-steps (45 B each at D = 8: >= 135 MB, half the Infinity Cache).
 // Same-box A/B (profiles/ab/r2_nt_out_ab.txt): config 3 447 vs 470 us per 10-step launch,
 // config 4 74-75 vs 94 us, single-step launches at config 3 52 vs 70 us; config 1 (200k
-// agent-steps, latency-bound) 8.2 vs 7.7 us, so small launches keep plain stores.
+// agent-steps, latency-bound) 8.2 vs 7.7 us, so small calls keep plain stores.
 #ifndef FENV_NT_OUT
 #define FENV_NT_OUT 1
 #endif
 constexpr double kNTMinAgentSteps = 3.0e6;
-static inline bool use_nt(const Consts &c, int32_t T) {
+bool rollout_nt(const Consts &c, int64_t T) {
     return FENV_NT_OUT && (double)c.F * (double)c.N * (double)T >= kNTMinAgentSteps;
+}
+// Steps per kernel launch of a large call.  With non-temporal stores, launches of <= 4 steps
+// stream at 0.89 of the HBM spec at config 3 against 0.69-0.70 for 6-10 (five steps is
+// address-dependent: either): the T output planes written concurrently by a launch are what the
+// memory system handles badly, so long calls run as short launches and pay the state round trip
+// (16 B per agent per launch) instead (profiles/ab/r2_chunk_ab.txt).  0: one launch per call.
+#ifndef FENV_LAUNCH_CHUNK
+#define FENV_LAUNCH_CHUNK 0
+#endif
+int32_t rollout_launch_steps(const Consts &c, int64_t T) {
+    if (FENV_LAUNCH_CHUNK <= 0 || !rollout_nt(c, T) || large_path(c.N)) return (int32_t)T;
+    return T < FENV_LAUNCH_CHUNK ? (int32_t)T : FENV_LAUNCH_CHUNK;
 }
 
 template <int D, int MODE>
 static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                              const float *act, float *obs, float *rew, uint8_t *done,
-                             float *partial, bool accum, hipStream_t st, const ActGen *gen) {
-    return use_nt(c, T) ? rollout_dmn<D, MODE, true>(c, s, p, T, act, obs, rew, done, partial,
-                                                     accum, st, gen)
-                        : rollout_dmn<D, MODE, false>(c, s, p, T, act, obs, rew, done, partial,
-                                                      accum, st, gen);
+                             float *partial, bool accum, bool nt, hipStream_t st,
+                             const ActGen *gen) {
+    return nt ? rollout_dmn<D, MODE, true>(c, s, p, T, act, obs, rew, done, partial, accum, st,
+                                           gen)
+              : rollout_dmn<D, MODE, false>(c, s, p, T, act, obs, rew, done, partial, accum, st,
+                                            gen);
 }
 
 const char *rollout_kernel_name(const Consts &c, int32_t T) {
@@ -831,18 +844,19 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
 
 hipError_t launch_rollout(const Consts &c, const DevState &s, const DevPending &p, int32_t T,
                           int32_t D, const float *act, float *obs, float *rew, uint8_t *done,
-                          float *partial, bool accum, hipStream_t st, const ActGen *gen) {
+                          float *partial, bool accum, bool nt, hipStream_t st,
+                          const ActGen *gen) {
     if (large_path(c.N))
         return launch_rollout_large(c, s, p, T, D, act, obs, rew, done, partial, accum, st, gen);
     const bool mt = c.reset_mode == FENV_RESET_MT19937;
     if (D == 8)
         return mt ? rollout_dm<8, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial,
-                                                      accum, st, gen)
+                                                      accum, nt, st, gen)
                   : rollout_dm<8, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial,
-                                                     accum, st, gen);
-    return mt ? rollout_dm<6, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial, accum,
+                                                     accum, nt, st, gen);
+    return mt ? rollout_dm<6, FENV_RESET_MT19937>(c, s, p, T, act, obs, rew, done, partial, accum, nt,
                                                   st, gen)
-              : rollout_dm<6, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial, accum,
+              : rollout_dm<6, FENV_RESET_PHILOX>(c, s, p, T, act, obs, rew, done, partial, accum, nt,
                                                  st, gen);
 }
 
