@@ -142,10 +142,27 @@ __device__ __forceinline__ float col_sum(const float *z, int B) {
 #endif
 }
 
+// Sum over the 64 lanes, in every lane.  FENV_PPO_DPP_SUM (default): DPP row shifts and row
+// broadcasts (a fixed order; six VALU ops and one v_readlane) instead of six dependent
+// ds_bpermute round trips of the xor butterfly.
+#ifndef FENV_PPO_DPP_SUM
+#define FENV_PPO_DPP_SUM 1
+#endif
 __device__ __forceinline__ float wsum(float v) {
+#if FENV_PPO_DPP_SUM
+    int x = __float_as_int(v);
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false)));
+    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+#else
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     return v;
+#endif
 }
 
 // unroll of the two 32-step fp32 MFMA loops (layer-2 forward; W2 grads + dL/dh1)
@@ -390,10 +407,23 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *a = H2 + (net * kPB + 16 * bt + c) * kRow + q;
                 const int hw = net ? L.valW : L.actW + (c & 1) * kHid;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (SPLIT) {  // operands read up front, branch-free (see head grads)
+                    float av[16], wv[16];
 #pragma unroll
-                for (int s4 = 0; s4 < 16; ++s4) {
-                    const float bw = c < ncol ? W[lx(hw + 4 * s4 + q)] : 0.0f;
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4], bw, acc, 0, 0, 0);
+                    for (int s4 = 0; s4 < 16; ++s4) {
+                        av[s4] = a[4 * s4];
+                        wv[s4] = W[lx(hw + 4 * s4 + q)];
+                    }
+#pragma unroll
+                    for (int s4 = 0; s4 < 16; ++s4)
+                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], c < ncol ? wv[s4] : 0.0f,
+                                                                  acc, 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int s4 = 0; s4 < 16; ++s4) {
+                        const float bw = c < ncol ? W[lx(hw + 4 * s4 + q)] : 0.0f;
+                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4], bw, acc, 0, 0, 0);
+                    }
                 }
                 if (c < ncol) {
                     const float hb = W[lx(net ? L.valb : L.actb + c)];
@@ -487,7 +517,49 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // dL/dz2 in place over the SAME H2 columns (only this wave reads or writes them in
             // this phase, so no barrier between); rows b >= B are zeroed so the contractions
             // over all 64 samples ignore them
-            {
+            if constexpr (SPLIT) {
+                // one wave per SIMD and a 512-register budget: every LDS operand of the phase is
+                // read up front (one wait instead of one per step) and the dL/dz2 loop is
+                // branch-free (rows b >= B select 0); same operations as the unsplit form below
+                const int net = w >> 2, kt = w & 3, q = lane >> 4, c = lane & 15;
+                const int ncol = net ? 1 : 2;
+                float *hcol = H2 + net * kPB * kRow + 16 * kt;
+                const float *sg = S + (net ? sGV : sGMU0 + (c & 1)) * kPB;
+                const float *s0p = S + (net ? sGV : sGMU0) * kPB, *s1p = S + sGMU1 * kPB;
+                float ha[16], sb[16], s0[16], s1[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int b = 4 * t + q;
+                    ha[t] = hcol[b * kRow + c];
+                    sb[t] = sg[b];
+                    s0[t] = s0p[b];
+                    s1[t] = net ? 0.0f : s1p[b];
+                }
+                const int k = 16 * kt + c;
+                const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
+                const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[t], c < ncol ? sb[t] : 0.0f, acc,
+                                                              0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int b = 4 * t + q;
+                    const float gh = net ? s0[t] * wa0 : s0[t] * wa0 + s1[t] * wa1;
+                    const float hv = ha[t];
+                    const float dz = gh * (1.0f - hv * hv);
+                    hcol[b * kRow + c] = b < B ? dz : 0.0f;
+                }
+                if (c < ncol) {
+                    const int hw = net ? L.valW : L.actW + c * kHid;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        G[lx(hw + 16 * kt + 4 * q + r)] = acc[r];
+                        gss = __builtin_fmaf(acc[r], acc[r], gss);
+                    }
+                }
+            } else {
                 const int net = w >> 2, kt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
                 float *hcol = H2 + net * kPB * kRow + 16 * kt;
@@ -612,12 +684,26 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int net = w >> 2, jt = w & 3, q = lane >> 4, c = lane & 15;
                 const float *Z1 = H1 + net * kPB * kRow + 16 * jt + c;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (SPLIT) {  // operands read up front, branch-free (see head grads)
+                    float zv[16], ov[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int b = 16 * q + i;
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Z1[b * kRow],
-                                                              c < 8 ? O[b * 9 + c] : 0.0f, acc,
-                                                              0, 0, 0);
+                    for (int i = 0; i < 16; ++i) {
+                        const int b = 16 * q + i;
+                        zv[i] = Z1[b * kRow];
+                        ov[i] = O[b * 9 + (c & 7)];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[i], c < 8 ? ov[i] : 0.0f, acc,
+                                                                  0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int b = 16 * q + i;
+                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Z1[b * kRow],
+                                                                  c < 8 ? O[b * 9 + c] : 0.0f, acc,
+                                                                  0, 0, 0);
+                    }
                 }
                 if (c < D) {
                     const int w1 = (net ? L.vf0W : L.pi0W) + (16 * jt + 4 * q) * D + c;
