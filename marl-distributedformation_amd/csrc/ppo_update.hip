@@ -243,13 +243,16 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         v[q] = p < P ? g.exp_avg_sq[p] : 0.0f;
     }
     float step = g.step[0];
-    // split: the LDS index of each Adam slot's parameter (-1: none), fixed for the launch
+    // split: the LDS index of each Adam slot's parameter, fixed for the launch; a slot without a
+    // parameter points at the pad float after parameter 63 (lx leaves one after every 64; no
+    // read ever uses it), so the Adam loop runs branch-free
+    constexpr int kPadIx = 64;
     int lp[SPLIT ? KP : 1];
     if constexpr (SPLIT) {
 #pragma unroll
         for (int q = 0; q < KP; ++q) {
             const int p = own(q);
-            lp[q] = p < P ? lx(p) : -1;
+            lp[q] = p < P ? lx(p) : kPadIx;
         }
     }
     bool partner_lost = false;  // split launch: the other block's norm exchange timed out
@@ -734,8 +737,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if constexpr (SPLIT) {
 #pragma unroll
                 for (int q = 0; q < KP; ++q) {
-                    gq[q] = lp[q] >= 0 ? G[lp[q]] : 0.0f;
-                    wq[q] = lp[q] >= 0 ? W[lp[q]] : 0.0f;
+                    gq[q] = G[lp[q]];
+                    wq[q] = W[lp[q]];
                 }
             }
             float tot = 0.f;
@@ -780,7 +783,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             const float inv_bc2s = 1.0f / __builtin_sqrtf(bc2);
 #pragma unroll
             for (int q = 0; q < KP; ++q) {
-                const int p = SPLIT ? (lp[q] >= 0 ? 0 : P) : own(q);
+                const int p = SPLIT ? 0 : own(q);  // split: every slot (spare ones hit the pad)
                 if (p < P) {
                     const int ix = SPLIT ? lp[q] : lx(p);
                     const float gr = (SPLIT ? gq[q] : G[ix]) * coef;
