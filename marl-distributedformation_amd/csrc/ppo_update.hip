@@ -178,6 +178,13 @@ __device__ __forceinline__ float wsum(float v) {
 #ifndef FENV_PPO_RING_L2
 #define FENV_PPO_RING_L2 8  // > 0: the same for the layer-2 forward loop
 #endif
+// ring depths of the split launch (one wave per SIMD: a 512-register budget)
+#ifndef FENV_PPO_RING_SPLIT
+#define FENV_PPO_RING_SPLIT 32
+#endif
+#ifndef FENV_PPO_RING_L2_SPLIT
+#define FENV_PPO_RING_L2_SPLIT 32
+#endif
 #ifndef FENV_PPO_DUMP_GRAD
 #define FENV_PPO_DUMP_GRAD 0
 #endif
@@ -373,7 +380,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
 #if FENV_PPO_RING_L2
-                constexpr int RL = FENV_PPO_RING_L2;
+                constexpr int RL = SPLIT ? FENV_PPO_RING_L2_SPLIT : FENV_PPO_RING_L2;
                 float ra[RL], rb[RL];
 #pragma unroll
                 for (int j = 0; j < RL; ++j) {
@@ -617,7 +624,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 for (int r = 0; r < 16; ++r) gw[r] = dz[r] = 0.0f;
 #if FENV_PPO_RING
                 // operands of step i + RD loaded while steps i.. issue (RD-deep register ring)
-                constexpr int RD = FENV_PPO_RING;
+                constexpr int RD = SPLIT ? FENV_PPO_RING_SPLIT : FENV_PPO_RING;
                 const float *pa = Z2 + (32 * h) * kRow + 32 * mt + c;
                 const float *pb = A1 + (32 * h) * kRow + 32 * nt + c;
                 const float *pc = Z2 + (32 * mt + c) * kRow + 32 * h;
