@@ -321,6 +321,15 @@ def random_action_bench(pkgname: str, dev, formations: int, agents: int, launche
             "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def secondary(fn, *a):
+    """A secondary line (after the timed region): an error in it is reported in its own field
+    instead of taking the headline line down with it."""
+    try:
+        return fn(*a)
+    except Exception as ex:
+        return {"error": f"{type(ex).__name__}: {ex}"}
+
+
 def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
                      updates: int = 2) -> dict:
     """Secondary measurement: SB3's PPO.train at the reference's training config
@@ -356,6 +365,7 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
             "ms_per_update": el / updates * 1e3, "us_per_minibatch": per_mb * 1e6,
             "samples_per_s": n * m.cfg.n_epochs / (el / updates),
             "gflops": flop / per_mb / 1e9,
+            "exchange_reruns": m.exchange_retries,
             "note": "actor and critic on one CU each (a minibatch depends on the previous "
                     "one's parameters); one CU's fp32 peak is ~614 GFLOP/s"}
 
@@ -673,9 +683,10 @@ def main():
                                     "agent_dones_sampled_rollout": t[1],
                                     "every_launches": stat_every}
         if world == 1 and not args.no_policy:
-            out["policy_rollout"] = policy_rollout_bench(pkg.__name__, dev, 65536, 10, 10)
+            out["policy_rollout"] = secondary(policy_rollout_bench, pkg.__name__, dev, 65536, 10,
+                                              10)
         if world == 1 and not args.no_policy:
-            out["ppo_update"] = ppo_update_bench(pkg.__name__, dev)
+            out["ppo_update"] = secondary(ppo_update_bench, pkg.__name__, dev)
         if world == 1 and not args.no_configs:
             out["random_action_rollout"] = random_action_bench(pkg.__name__, dev,
                                                                args.formations, N)

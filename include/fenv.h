@@ -210,7 +210,8 @@ int fenv_policy_rollout(fenv_t *env, const float *params, int32_t T, uint64_t se
 
 /* ------------------------------------------------------------------ PPO update
  * SB3 2.x PPO.train for small minibatches (batch_size <= 64, the SB3 default under
- * vectorized_env.py:126-131) in ONE single-workgroup launch: for each of n_epochs, the n
+ * vectorized_env.py:126-131) in ONE launch (the actor and the critic on one workgroup each,
+ * exchanging their gradient-norm partials once per minibatch): for each of n_epochs, the n
  * samples in the order perm[epoch][0..n) split into minibatches of batch_size (the last one
  * partial); per minibatch the clipped surrogate + vf_coef * MSE(returns, values) + ent_coef *
  * entropy loss (advantages normalised per minibatch when normalize_advantage), backward,
@@ -218,7 +219,9 @@ int fenv_policy_rollout(fenv_t *env, const float *params, int32_t T, uint64_t se
  * policy_forward layout) are updated in place; exp_avg / exp_avg_sq [P] and *step (one float)
  * are the Adam state (device); stats (device, 4 doubles) are INCREMENTED by the per-minibatch
  * policy loss, value loss, entropy loss and clip fraction.  Sample buffers (device): obs [n][D],
- * actions [n][2] (unclipped), old_log_prob, advantages, returns [n]; perm int64 [n_epochs][n]. */
+ * actions [n][2] (unclipped), old_log_prob, advantages, returns [n]; perm int64 [n_epochs][n].
+ * If the two workgroups' exchange times out (a workgroup never became resident), the update
+ * leaves NaN parameters and marks stats: stats[0] NaN and stats[3] below -1e29. */
 typedef struct ppo_hparams {
     float clip_range, ent_coef, vf_coef, max_grad_norm, lr, beta1, beta2, eps;
     int32_t normalize_advantage;

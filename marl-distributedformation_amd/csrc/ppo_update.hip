@@ -189,7 +189,7 @@ __device__ __forceinline__ float wsum(float v) {
 #define FENV_PPO_DUMP_GRAD 0
 #endif
 #ifndef FENV_PPO_PROFILE
-#define FENV_PPO_PROFILE 0  // 1: per-phase shader-clock totals -> stats[4..15] (diagnostic build)
+#define FENV_PPO_PROFILE 0  // 1 / 2: per-phase shader-clock totals of the actor / critic block -> stats[4..15] (diagnostic build)
 #endif
 #if FENV_PPO_PROFILE
 #define FENV_PPO_PHASE(i)                                            \
@@ -314,6 +314,20 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         load_rows(ro0, rs0, po, ps);
         perm_rows(1, ro_n, rs_n);
     }
+    // Advantage normalisation of a Bk-sample minibatch (whole wave; lane l < Bk holds sample
+    // l's advantage a).  It depends on the data only, so the split launch's actor block does it
+    // one minibatch ahead, while its norm exchange waits on L2 (adv_nx: wave 0's lanes).
+    auto adv_norm = [&](int Bk, float a) -> float {
+        if (!(hp.normalize_advantage && Bk > 1)) return a;
+        const float invBk = 1.0f / (float)Bk;
+        const float x = lane < Bk ? a : 0.0f;
+        const float mean = wsum(x) * invBk;
+        const float d = lane < Bk ? x - mean : 0.0f;
+        const float sd = __builtin_sqrtf(wsum(d * d) / (float)(Bk - 1));
+        return (x - mean) / (sd + 1e-8f);
+    };
+    float adv_nx = 0.0f;
+    if (SPLIT && net_b == 0 && wl == 0) adv_nx = adv_norm((int)(n < bs ? n : bs), ps[3]);
     int64_t kmb = 0;
     for (int ep = 0; ep < g.n_epochs; ++ep) {
         for (int64_t s0 = 0; s0 < n; s0 += bs, ++kmb) {
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 S[sA0 * kPB + tid] = ps[0];
                 S[sA1 * kPB + tid] = ps[1];
                 S[sOLP * kPB + tid] = ps[2];
-                S[sADV * kPB + tid] = ps[3];
+                S[sADV * kPB + tid] = (SPLIT && net_b == 0) ? adv_nx : ps[3];
                 S[sRET * kPB + tid] = ps[4];
             }
             load_rows(ro_n, rs_n, po, ps);
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             __syncthreads();
             FENV_PPO_PHASE(0);
             // ---- advantage normalisation (wave 0) || layer 1 (all waves)
-            if (w == 0 && hp.normalize_advantage && B > 1) {
+            if (!SPLIT && w == 0 && hp.normalize_advantage && B > 1) {
                 const float a = lane < B ? S[sADV * kPB + lane] : 0.0f;
                 const float mean = wsum(a) * invB;
                 const float d = lane < B ? a - mean : 0.0f;
@@ -754,22 +768,36 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 // the other network's partial (actor's first in the sum on both blocks).  The
                 // wait is bounded: a missing partner poisons the update with NaN instead of
                 // hanging the GPU.
+                const uint64_t seq = (uint64_t)(kmb + 1);
+                uint64_t o = 0;
                 if (tid == 0) {
-                    const uint64_t seq = (uint64_t)(kmb + 1);
                     // one 64-bit word carries both the value and its sequence number, so relaxed
                     // device-scope atomics suffice (nothing else is published through it)
-                    __hip_atomic_store(g.xch + net_b, (seq << 32) | __float_as_uint(tot),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    uint64_t o = 0;
+                    // two words per block, by minibatch parity: the partner's word for this
+                    // minibatch cannot be overwritten before this block has read it (its next
+                    // post to the same word is two minibatches on, which waits on this block)
+                    __hip_atomic_store(g.xch + 2 * net_b + (kmb & 1),
+                                       (seq << 32) | __float_as_uint(tot), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    if (!partner_lost)
+                        o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
+                // at this minibatch's gather) while the first load is in flight
+                if (net_b == 0 && wl == 0 && kmb + 1 < nmb) {
+                    const int64_t k1 = kmb + 1, e1 = k1 / kMB, s1 = (k1 - e1 * kMB) * bs;
+                    adv_nx = adv_norm((int)((n - s1) < bs ? (n - s1) : bs), ps[3]);
+                }
+                if (tid == 0) {
                     // after one timed-out wait the partner is taken as lost for good: no further
                     // waits, so a broken launch ends in milliseconds, not one timeout per
                     // minibatch
                     const int max_spin = partner_lost ? 0 : (1 << 22);
-                    for (int spin = 0; spin < max_spin; ++spin) {
-                        o = __hip_atomic_load(g.xch + (net_b ^ 1), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-                        if ((o >> 32) == seq) break;
+                    for (int spin = 0; spin < max_spin && (o >> 32) != seq; ++spin) {
                         __builtin_amdgcn_s_sleep(1);
+                        o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     partner_lost = (o >> 32) != seq;
                     const float other = partner_lost ? __builtin_nanf("") : __uint_as_float((uint32_t)o);
@@ -828,18 +856,24 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     }
     if (tid == 0 && net_b == 0) {
         g.step[0] = step;
-        g.stats[0] += st_pl;
+        atomicAdd(g.stats + 0, st_pl);  // atomic: the other block may mark a lost exchange
         if (!SPLIT) g.stats[1] += st_vl;
         g.stats[2] += st_el;
-        g.stats[3] += st_cf;
-#if FENV_PPO_PROFILE
+        atomicAdd(g.stats + 3, st_cf);
+    }
+#if FENV_PPO_PROFILE  // 1: the actor block's phases, 2: the critic block's (split launch)
+    if (tid == 0 && net_b == (FENV_PPO_PROFILE == 2 ? 1 : 0))
         for (int q = 0; q < 11; ++q) g.stats[4 + q] += prof[q];
 #endif
-    }
     if (SPLIT && tid == 0 && net_b == 1) g.stats[1] += st_vl;
-    // split: a norm exchange that timed out leaves NaN parameters; say so in the policy-loss
-    // slot too, which the host checks (ppo.py raises)
-    if (SPLIT && tid == 0 && partner_lost) g.stats[0] = __builtin_nan("");
+    // split: a norm exchange that timed out leaves NaN parameters; say so in the stats, which the
+    // host checks (ppo.py).  Atomic adds, so the mark survives in whichever order the two blocks
+    // write: NaN policy-loss sum, and a clip-fraction sum far below zero (a lost partner, not
+    // divergence)
+    if (SPLIT && tid == 0 && partner_lost) {
+        atomicAdd(g.stats + 0, (double)__builtin_nanf(""));
+        atomicAdd(g.stats + 3, -1e30);
+    }
 }
 
 hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
@@ -859,19 +893,19 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
     }
     uint64_t *xch = nullptr;
     if (split) {
-        // exchange words, one pair per device, cleared before every launch (sequence numbers
-        // restart at 1)
-        static uint64_t *words[64] = {};  // 16 B per device, kept for the process lifetime
+        // exchange words, two per block and device, cleared before every launch (sequence
+        // numbers restart at 1)
+        static uint64_t *words[64] = {};  // 32 B per device, kept for the process lifetime
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
         if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
         if (!words[dev]) {
-            e = hipMalloc(&words[dev], 2 * sizeof(uint64_t));
+            e = hipMalloc(&words[dev], 4 * sizeof(uint64_t));
             if (e != hipSuccess) return e;
         }
         xch = words[dev];
-        e = hipMemsetAsync(xch, 0, 2 * sizeof(uint64_t), st);
+        e = hipMemsetAsync(xch, 0, 4 * sizeof(uint64_t), st);
         if (e != hipSuccess) return e;
         const PLayout L(D);
         if ((L.vf0W - L.pi0W) + (L.valW - L.actW) + 2 > kPTS * kPerTS ||

@@ -142,6 +142,7 @@ class PPO:
         self._perm = torch.zeros(n, dtype=torch.long, device=dev)
         self._k = torch.zeros((), dtype=torch.long, device=dev)
         self._sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.exchange_retries = 0  # fused update launches re-run after a lost norm exchange
         self._graphs = None
         # batch_size <= 64 (SB3's default 64): the whole update as one HIP kernel (ppo_update)
         self.use_fused = ((self.param.device.type == "cuda" and self.cfg.batch_size <= 64)
@@ -264,17 +265,28 @@ class PPO:
                              max_grad_norm=c.max_grad_norm, lr=float(grp["lr"]),
                              beta1=float(grp["betas"][0]), beta2=float(grp["betas"][1]),
                              eps=float(grp["eps"]), normalize_advantage=int(c.normalize_advantage))
-        self._sums.zero_()
-        _lib.check(_lib.lib().ppo_update(
-            _lib.ptr(self.param), _lib.ptr(st["exp_avg"]), _lib.ptr(st["exp_avg_sq"]),
-            _lib.ptr(st["step"]), self.buffer.obs_dim, _lib.ptr(obs), _lib.ptr(act), _lib.ptr(lp),
-            _lib.ptr(adv), _lib.ptr(ret), n, _lib.ptr(perm), c.n_epochs, bs,
-            ctypes.byref(hp), _lib.ptr(self._sums), _lib.current_stream(dev)), "ppo_update")
+        state = (self.param, st["exp_avg"], st["exp_avg_sq"], st["step"])
+        snap = tuple(t.detach().clone() for t in state)  # ~120 KB: restored if the launch is lost
         steps = c.n_epochs * (-(-n // bs))
-        m = (self._sums / steps).tolist()
+        for attempt in range(2):
+            self._sums.zero_()
+            _lib.check(_lib.lib().ppo_update(
+                _lib.ptr(self.param), _lib.ptr(st["exp_avg"]), _lib.ptr(st["exp_avg_sq"]),
+                _lib.ptr(st["step"]), self.buffer.obs_dim, _lib.ptr(obs), _lib.ptr(act),
+                _lib.ptr(lp), _lib.ptr(adv), _lib.ptr(ret), n, _lib.ptr(perm), c.n_epochs, bs,
+                ctypes.byref(hp), _lib.ptr(self._sums), _lib.current_stream(dev)), "ppo_update")
+            m = (self._sums / steps).tolist()
+            if not (math.isnan(m[0]) and m[3] < 0):
+                break
+            # the two workgroups' norm exchange timed out (include/fenv.h): restore, run again
+            self.exchange_retries += 1
+            with torch.no_grad():
+                for t, s in zip(state, snap):
+                    t.copy_(s)
         if math.isnan(m[0]):
-            raise RuntimeError("fused PPO update: NaN policy loss (the update diverged, or the "
-                               "two-CU launch's gradient-norm exchange timed out)")
+            raise RuntimeError("fused PPO update: NaN policy loss (" +
+                               ("the two-CU launch's gradient-norm exchange timed out twice)"
+                                if m[3] < 0 else "the update diverged)"))
         self.stats = dict(policy_gradient_loss=m[0], value_loss=m[1], entropy_loss=m[2],
                           clip_fraction=m[3])
         return self.stats
