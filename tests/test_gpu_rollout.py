@@ -226,6 +226,41 @@ def test_fused_update_matches_torch(mods, goal):
         assert abs(s0[k] - s1[k]) <= 1e-4 * max(1.0, abs(s0[k])), (k, s0[k], s1[k])
 
 
+def test_fused_update_repeatable(mods):
+    """The two-CU fused update (actor and critic blocks exchanging the gradient norm through L2
+    every minibatch) is deterministic: 8 launches from the same parameters / Adam state / samples
+    at the reference's training config (1000 x 5 agents, 10 epochs x 782 minibatches) give
+    bit-identical parameters, Adam moments and loss sums, with no launch re-run after a lost
+    exchange (ppo.py exchange_retries, profiles/ab/r2_ppo_exchange_ab.txt)."""
+    cfg = {"num_formation": 1000, "num_agents_per_formation": 5, "goal_in_obs": True}
+    env = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=2, reset_mode="philox")
+    ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(), seed=3, use_graph=False, use_fused=True)
+    with torch.no_grad():
+        ppo.collector.collect()
+    ppo.train()  # creates the Adam state
+    with torch.no_grad():
+        ppo.collector.collect()
+    st = ppo.opt.state[ppo.param]
+    state = (ppo.param, st["exp_avg"], st["exp_avg_sq"], st["step"])
+    snap = tuple(t.detach().clone() for t in state)
+    gen = ppo.gen.get_state()  # the epochs' permutations are drawn from it
+    ref = None
+    for r in range(8):
+        with torch.no_grad():
+            for t, s in zip(state, snap):
+                t.copy_(s)
+        ppo.gen.set_state(gen)
+        stats = ppo.train()
+        out = tuple(t.detach().clone() for t in state) + (stats,)
+        if ref is None:
+            ref = out
+            continue
+        for k in range(4):
+            assert torch.equal(out[k], ref[k]), (r, k)
+        assert out[4] == ref[4], r
+    assert ppo.exchange_retries == 0
+
+
 @pytest.mark.parametrize("mode", ["mt19937", "philox"])
 def test_sharded_rollouts_concatenate_to_unsharded(mods, mode):
     """Shards of one batch (uneven: 26 + 25 formations) collect, between them, exactly the
