@@ -786,7 +786,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
                 // at this minibatch's gather) while the first load is in flight
                 if (net_b == 0 && wl == 0 && kmb + 1 < nmb) {
-                    const int64_t k1 = kmb + 1, e1 = k1 / kMB, s1 = (k1 - e1 * kMB) * bs;
+                    const int64_t s1 = s0 + bs < n ? s0 + bs : 0;  // next minibatch's start
                     adv_nx = adv_norm((int)((n - s1) < bs ? (n - s1) : bs), ps[3]);
                 }
                 if (tid == 0) {
