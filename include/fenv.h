@@ -29,6 +29,15 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header.  A host program compiled against one revision checks
+ * fenv_abi_version() == FENV_ABI_VERSION at start-up: a signature that changed between revisions
+ * gets a new symbol name, never a reordered argument list under the old one.
+ *   1  round-1/2 entry points (policy_forward with row0)
+ *   2  + fenv_abi_version, fenv_get_state_range, fenv_metrics_range, ppo_workspace_bytes,
+ *        ppo_update_ws, ppo_grad, ppo_apply */
+#define FENV_ABI_VERSION 2
+int fenv_abi_version(void);
+
 typedef struct fenv fenv_t;
 
 enum {
@@ -62,6 +71,11 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
                 int32_t goal_in_obs, double share_reward_ratio, int32_t max_steps, uint32_t seed,
                 int32_t reset_mode, int64_t first_formation, int64_t total_formations);
 
+/* Frees the handle and every device/pinned buffer it owns.  Safe at any point: it restores the
+ * caller's current device, waits for the handle's own staging copy (hipFree then waits for the
+ * device's work), and a free that the runtime refuses because a stream capture is under way is
+ * parked and retried by the next fenv_create / fenv_destroy.  A second destroy of the same
+ * handle is detected where the memory still holds it and returns FENV_EINVAL. */
 int fenv_destroy(fenv_t *env);
 
 /* out_host[0..7] = {num_formation, num_agents, obs_dim, num_agents_total(A), steps_since_reset
@@ -132,6 +146,16 @@ int fenv_get_state(fenv_t *env, float *px, float *py, float *gx, float *gy, int3
                    void *stream);
 int fenv_set_state(fenv_t *env, const float *px, const float *py, const float *gx,
                    const float *gy, const int32_t *t, void *stream);
+
+/* One formation range [first, first + count) of the handle's shard (FormationEnv.formationsim_list
+ * [i], vectorized_env.py:38-43 / simulate.py:133-147): fenv_get_state's buffers for those
+ * formations only -- px,py [count*N], gx,gy,t [count] -- so a view costs O(count*N), not O(A). */
+int fenv_get_state_range(fenv_t *env, int64_t first, int64_t count, float *px, float *py,
+                         float *gx, float *gy, int32_t *t, void *stream);
+/* fenv_metrics over formations [first, first + count) only: rew [count*N] (may be NULL),
+ * out [count][8], sums [8] (may be NULL).  Values equal the matching rows of fenv_metrics. */
+int fenv_metrics_range(fenv_t *env, int64_t first, int64_t count, const float *rew, float *out,
+                       double *sums, void *stream);
 
 /* Host-only (no GPU needed): the reset positions the reference's global MT19937 stream gives
  * formations [first, first+count) of a draw set of `total` formations that starts `skip_sets`
@@ -231,6 +255,38 @@ int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, in
                const float *advantages, const float *returns, int64_t n, const int64_t *perm,
                int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
                void *stream);
+/* ppo_update with caller-owned exchange words: workspace = ppo_workspace_bytes() of device memory
+ * owned by one PPO instance (cleared by each launch on `stream`).  Concurrent updates on
+ * different streams must use different workspaces.  (ppo_update itself takes a stream-ordered
+ * allocation of its own per launch, hipMallocAsync/hipFreeAsync, so it is safe too.) */
+int64_t ppo_workspace_bytes(void);
+int ppo_update_ws(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
+                  const float *obs, const float *actions, const float *old_log_prob,
+                  const float *advantages, const float *returns, int64_t n, const int64_t *perm,
+                  int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
+                  void *workspace, void *stream);
+
+/* Data-parallel PPO update ("RCCL ... all-reducing policy gradients"), one
+ * global minibatch at a time, each rank holding b_local of its b_global samples:
+ *   ppo_grad  -- this rank's share of the minibatch loss gradient on the fused kernel (one
+ *                launch, the actor and critic on one CU each): the rows `rows[b_local]` of the
+ *                sample buffers (layouts as ppo_update), loss means taken over b_global samples,
+ *                advantages normalised with the GLOBAL minibatch's adv_mean / adv_std (when
+ *                adv_normalize and b_global > 1), the entropy term included only when
+ *                entropy_term (one rank).  grad [P] is overwritten (unclipped); stats [4] are
+ *                INCREMENTED by this rank's share of the four loss means (as ppo_update's).
+ *                b_local = 0 writes a zero gradient (plus the entropy term if entropy_term).
+ *   (the caller all-reduces grad, SUM, over the ranks)
+ *   ppo_apply -- clip_grad_norm_(max_grad_norm) + Adam (torch's capturable-Adam operation
+ *                order) from the reduced gradient; params / exp_avg / exp_avg_sq / *step as
+ *                ppo_update.  Every rank applies the same reduced gradient to the same state. */
+int ppo_grad(const float *params, int32_t obs_dim, const float *obs, const float *actions,
+             const float *old_log_prob, const float *advantages, const float *returns,
+             const int64_t *rows, int32_t b_local, int32_t b_global, float adv_mean,
+             float adv_std, int32_t adv_normalize, int32_t entropy_term, const ppo_hparams *hp,
+             float *grad, double *stats, void *stream);
+int ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, float *step, const float *grad,
+              int32_t obs_dim, const ppo_hparams *hp, void *stream);
 
 const char *fenv_last_error(void);
 

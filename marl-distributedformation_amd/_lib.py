@@ -44,6 +44,9 @@ SIGNATURES = {
     "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
     "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),
     "fenv_get_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
+    "fenv_get_state_range": (_I32, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P]),
+    "fenv_metrics_range": (_I32, [_P, _I64, _I64, _P, _P, _P, _P]),
+    "fenv_abi_version": (_I32, []),
     "fenv_set_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
     "fenv_host_reset_draws": (_I32, [_U32, _I64, _I64, _I64, _I64, _I32, _P, _P, _P, _P]),
     "fenv_desired_neighbor_dist": (ctypes.c_float, [_I32]),
@@ -57,6 +60,12 @@ SIGNATURES = {
                                    ctypes.c_float, _P, _P]),
     "ppo_update": (_I32, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P, _I32, _I32, _P,
                           _P, _P]),
+    "ppo_workspace_bytes": (_I64, []),
+    "ppo_update_ws": (_I32, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I64, _P, _I32, _I32, _P,
+                             _P, _P, _P]),
+    "ppo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.c_float,
+                        ctypes.c_float, _I32, _I32, _P, _P, _P, _P]),
+    "ppo_apply": (_I32, [_P, _P, _P, _P, _P, _I32, _P, _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
 
@@ -106,6 +115,30 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+_deferred: list = []
+
+
+def destroy_handle(h) -> None:
+    """``fenv_destroy`` of a handle, from release() or a finalizer.  While a HIP graph is being
+    captured on this thread's current stream the device frees inside it would invalidate the
+    capture, so the handle is parked and destroyed at the next create/destroy outside a capture
+    (the library also parks any free the runtime refuses, csrc/fenv_api.cpp)."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        _deferred.append(h)
+        return
+    flush_deferred()
+    check(lib().fenv_destroy(h), "fenv_destroy")
+
+
+def flush_deferred() -> None:
+    """Destroy the handles parked by :func:`destroy_handle` (no-op while capturing)."""
+    if not _deferred or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        return
+    L = lib()
+    while _deferred:
+        L.fenv_destroy(_deferred.pop())
 
 
 def check(rc: int, what: str = "") -> None:

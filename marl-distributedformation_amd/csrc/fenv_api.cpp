@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -51,9 +52,59 @@ inline void draw_formation(std::mt19937 &mt, int32_t N, float *px, float *py, fl
     gy = g1 * 480.0f + 60.0f;
 }
 
+// Device frees the runtime refused because a stream capture was under way (a hipFree inside a
+// capture is not allowed and would invalidate it): parked here, retried at the next
+// fenv_create / fenv_destroy, so fenv_destroy is safe to call at any point.
+struct Graveyard {
+    std::mutex mu;
+    std::vector<std::pair<int32_t, void *>> dev;   // (device, pointer) for hipFree
+    std::vector<std::pair<int32_t, void *>> host;  // for hipHostFree
+};
+Graveyard &graveyard() {
+    static Graveyard *g = new Graveyard();  // never destroyed: usable from atexit / finalizers
+    return *g;
+}
+bool capture_error(hipError_t e) {
+    return e == hipErrorStreamCaptureUnsupported || e == hipErrorStreamCaptureImplicit ||
+           e == hipErrorStreamCaptureInvalidated || e == hipErrorCapturedEvent;
+}
+void free_dev(int32_t device, void *p) {
+    if (!p) return;
+    if (capture_error(hipFree(p))) {
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> lk(graveyard().mu);
+        graveyard().dev.emplace_back(device, p);
+    }
+}
+void free_host(int32_t device, void *p) {
+    if (!p) return;
+    if (capture_error(hipHostFree(p))) {
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> lk(graveyard().mu);
+        graveyard().host.emplace_back(device, p);
+    }
+}
+// Retry the parked frees (each is parked again if a capture is still under way).
+void drain_graveyard() {
+    std::vector<std::pair<int32_t, void *>> dev, host;
+    {
+        std::lock_guard<std::mutex> lk(graveyard().mu);
+        dev.swap(graveyard().dev);
+        host.swap(graveyard().host);
+    }
+    for (auto &d : dev) {
+        (void)hipSetDevice(d.first);
+        free_dev(d.first, d.second);
+    }
+    for (auto &h : host) free_host(h.first, h.second);
+}
+
+constexpr uint64_t kLive = 0x666e65762d6c6976ull;  // "fenv-liv": a handle not yet destroyed
+
 }  // namespace
 
 struct fenv {
+    uint64_t magic = kLive;
     int32_t device = 0;
     fenvk::Consts c{};
     int32_t D = 8;
@@ -124,6 +175,8 @@ extern "C" {
 
 const char *fenv_last_error(void) { return g_err.c_str(); }
 
+int fenv_abi_version(void) { return FENV_ABI_VERSION; }
+
 float fenv_desired_neighbor_dist(int32_t num_agents) {
     // simulate.py:26 in float64 (numpy), rounded to fp32 where it meets the fp32 tensor.
     return (float)(2.0 * 60.0 * std::sin(M_PI / (double)num_agents));
@@ -151,6 +204,9 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     int ndev = 0;
     FENV_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(FENV_EINVAL, "device index out of range");
+    int prev_dev = -1;
+    FENV_HIP(hipGetDevice(&prev_dev));
+    drain_graveyard();
     FENV_HIP(hipSetDevice(device));
 
     fenv *e = new fenv();
@@ -176,6 +232,7 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
 
     auto cleanup = [&](int code) {
         fenv_destroy(e);
+        if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
         return code;
     };
     const size_t A = (size_t)e->A, F = (size_t)c.F;
@@ -216,21 +273,32 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     he = hipStreamSynchronize(nullptr);
     if (he != hipSuccess) return cleanup(fail(FENV_EHIP, hipGetErrorString(he)));
     *out = e;
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     return FENV_OK;
 }
 
 int fenv_destroy(fenv_t *e) {
     if (!e) return FENV_OK;
+    if (e->magic != kLive) return fail(FENV_EINVAL, "fenv_destroy: not a live handle (destroyed twice?)");
+    e->magic = 0;
+    // Safe at any point: the caller's current device is restored; the handle's own staging copy
+    // is waited for (hipFree then waits for the device's kernels); a free the runtime refuses
+    // during a stream capture is parked and retried later instead of failing the capture.
+    int prev = -1;
+    const bool have_prev = hipGetDevice(&prev) == hipSuccess;
     (void)hipSetDevice(e->device);
+    drain_graveyard();
     if (e->pend_ev_recorded) (void)hipEventSynchronize(e->pend_ev);
-    if (e->s.px) (void)hipFree(e->s.px);
-    if (e->pend) (void)hipFree(e->pend);
-    if (e->hpend) (void)hipHostFree(e->hpend);
+    free_dev(e->device, e->s.px);
+    free_dev(e->device, e->pend);
+    free_host(e->device, e->hpend);
     if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
-    if (e->lv_scratch) (void)hipFree(e->lv_scratch);
-    if (e->term) (void)hipFree(e->term);
-    if (e->lf) (void)hipFree(e->lf);
+    free_dev(e->device, e->lv_scratch);
+    free_dev(e->device, e->term);
+    free_dev(e->device, e->lf);
     delete e;
+    (void)hipGetLastError();  // leave no stale error for the caller's next error check
+    if (have_prev && prev >= 0) (void)hipSetDevice(prev);
     return FENV_OK;
 }
 
@@ -365,6 +433,41 @@ int fenv_get_state(fenv_t *e, float *px, float *py, float *gx, float *gy, int32_
     if (gx) FENV_HIP(hipMemcpyAsync(gx, e->s.gx, F * 4, hipMemcpyDeviceToDevice, st));
     if (gy) FENV_HIP(hipMemcpyAsync(gy, e->s.gy, F * 4, hipMemcpyDeviceToDevice, st));
     if (t) FENV_HIP(hipMemcpyAsync(t, e->s.t, F * 4, hipMemcpyDeviceToDevice, st));
+    return FENV_OK;
+}
+
+int fenv_get_state_range(fenv_t *e, int64_t first, int64_t count, float *px, float *py,
+                         float *gx, float *gy, int32_t *t, void *stream) {
+    if (!e) return fail(FENV_EINVAL, "fenv_get_state_range: NULL handle");
+    if (first < 0 || count < 1 || first + count > e->c.F)
+        return fail(FENV_EINVAL, "fenv_get_state_range: formations outside the handle's shard");
+    FENV_HIP(hipSetDevice(e->device));
+    hipStream_t st = as_stream(stream);
+    const size_t a0 = (size_t)first * e->c.N, na = (size_t)count * e->c.N, nf = (size_t)count;
+    if (px) FENV_HIP(hipMemcpyAsync(px, e->s.px + a0, na * 4, hipMemcpyDeviceToDevice, st));
+    if (py) FENV_HIP(hipMemcpyAsync(py, e->s.py + a0, na * 4, hipMemcpyDeviceToDevice, st));
+    if (gx) FENV_HIP(hipMemcpyAsync(gx, e->s.gx + first, nf * 4, hipMemcpyDeviceToDevice, st));
+    if (gy) FENV_HIP(hipMemcpyAsync(gy, e->s.gy + first, nf * 4, hipMemcpyDeviceToDevice, st));
+    if (t) FENV_HIP(hipMemcpyAsync(t, e->s.t + first, nf * 4, hipMemcpyDeviceToDevice, st));
+    return FENV_OK;
+}
+
+int fenv_metrics_range(fenv_t *e, int64_t first, int64_t count, const float *rew, float *out,
+                       double *sums, void *stream) {
+    if (!e || !out) return fail(FENV_EINVAL, "fenv_metrics_range: NULL argument");
+    if (first < 0 || count < 1 || first + count > e->c.F)
+        return fail(FENV_EINVAL, "fenv_metrics_range: formations outside the handle's shard");
+    FENV_HIP(hipSetDevice(e->device));
+    // the metrics kernels over a sub-shard: the same kernels on views of the state arrays
+    fenvk::Consts c = e->c;
+    c.F = count;
+    c.f0 = e->c.f0 + first;
+    const int64_t a0 = first * (int64_t)e->c.N;
+    fenvk::DevState s{e->s.px + a0, e->s.py + a0, e->s.gx + first, e->s.gy + first,
+                      e->s.t + first, e->s.ep + first};
+    fenvk::DevPending p = e->pending();
+    p.term += a0;
+    FENV_HIP(fenvk::launch_metrics(c, s, p, e->term_valid, rew, out, sums, as_stream(stream)));
     return FENV_OK;
 }
 
@@ -509,11 +612,12 @@ int rollout_gae(const float *rew, const float *values, const uint8_t *episode_st
     return FENV_OK;
 }
 
-int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
-               const float *obs, const float *actions, const float *old_log_prob,
-               const float *advantages, const float *returns, int64_t n, const int64_t *perm,
-               int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
-               void *stream) {
+static int ppo_update_impl(float *params, float *exp_avg, float *exp_avg_sq, float *step,
+                           int32_t obs_dim, const float *obs, const float *actions,
+                           const float *old_log_prob, const float *advantages,
+                           const float *returns, int64_t n, const int64_t *perm, int32_t n_epochs,
+                           int32_t batch_size, const ppo_hparams *hp, double *stats,
+                           void *workspace, void *stream) {
     if (!params || !exp_avg || !exp_avg_sq || !step || !obs || !actions || !old_log_prob ||
         !advantages || !returns || !perm || !hp || !stats)
         return fail(FENV_EINVAL, "ppo_update: NULL argument");
@@ -523,7 +627,68 @@ int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, in
     if (n_epochs == 0) return FENV_OK;
     FENV_HIP(fenvk::launch_ppo_update(params, exp_avg, exp_avg_sq, step, obs_dim, obs, actions,
                                       old_log_prob, advantages, returns, n, perm, n_epochs,
-                                      batch_size, *hp, stats, as_stream(stream)));
+                                      batch_size, *hp, stats, workspace, as_stream(stream)));
+    return FENV_OK;
+}
+
+int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
+               const float *obs, const float *actions, const float *old_log_prob,
+               const float *advantages, const float *returns, int64_t n, const int64_t *perm,
+               int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
+               void *stream) {
+    return ppo_update_impl(params, exp_avg, exp_avg_sq, step, obs_dim, obs, actions, old_log_prob,
+                           advantages, returns, n, perm, n_epochs, batch_size, hp, stats, nullptr,
+                           stream);
+}
+
+int64_t ppo_workspace_bytes(void) { return (int64_t)fenvk::ppo_workspace_bytes_impl(); }
+
+int ppo_update_ws(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
+                  const float *obs, const float *actions, const float *old_log_prob,
+                  const float *advantages, const float *returns, int64_t n, const int64_t *perm,
+                  int32_t n_epochs, int32_t batch_size, const ppo_hparams *hp, double *stats,
+                  void *workspace, void *stream) {
+    if (!workspace) return fail(FENV_EINVAL, "ppo_update_ws: NULL workspace");
+    return ppo_update_impl(params, exp_avg, exp_avg_sq, step, obs_dim, obs, actions, old_log_prob,
+                           advantages, returns, n, perm, n_epochs, batch_size, hp, stats,
+                           workspace, stream);
+}
+
+int ppo_grad(const float *params, int32_t obs_dim, const float *obs, const float *actions,
+             const float *old_log_prob, const float *advantages, const float *returns,
+             const int64_t *rows, int32_t b_local, int32_t b_global, float adv_mean,
+             float adv_std, int32_t adv_normalize, int32_t entropy_term, const ppo_hparams *hp,
+             float *grad, double *stats, void *stream) {
+    if (!params || !obs || !actions || !old_log_prob || !advantages || !returns || !hp ||
+        !grad || !stats || (b_local > 0 && !rows))
+        return fail(FENV_EINVAL, "ppo_grad: NULL argument");
+    if (obs_dim != 6 && obs_dim != 8) return fail(FENV_EINVAL, "ppo_grad: obs_dim must be 6 or 8");
+    if (b_local < 0 || b_local > 64 || b_global < 1 || b_local > b_global)
+        return fail(FENV_EINVAL, "ppo_grad: need 0 <= b_local <= min(64, b_global)");
+    hipStream_t st = as_stream(stream);
+    if (b_local == 0) {  // no rows here: a zero gradient (+ the entropy term if this rank owns it)
+        const int P = policy_param_count(obs_dim);
+        FENV_HIP(hipMemsetAsync(grad, 0, (size_t)P * sizeof(float), st));
+        if (entropy_term) {
+            const float e[2] = {-hp->ent_coef, -hp->ent_coef};
+            FENV_HIP(hipMemcpyAsync(grad + P - 2, e, sizeof(e), hipMemcpyHostToDevice, st));
+            FENV_HIP(hipStreamSynchronize(st));  // e is on the host stack
+        }
+        return FENV_OK;
+    }
+    FENV_HIP(fenvk::launch_ppo_grad(params, obs_dim, obs, actions, old_log_prob, advantages,
+                                    returns, rows, b_local, b_global, adv_mean, adv_std,
+                                    adv_normalize, entropy_term, *hp, grad, stats, st));
+    return FENV_OK;
+}
+
+int ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, float *step, const float *grad,
+              int32_t obs_dim, const ppo_hparams *hp, void *stream) {
+    if (!params || !exp_avg || !exp_avg_sq || !step || !grad || !hp)
+        return fail(FENV_EINVAL, "ppo_apply: NULL argument");
+    if (obs_dim != 6 && obs_dim != 8) return fail(FENV_EINVAL, "ppo_apply: obs_dim must be 6 or 8");
+    FENV_HIP(fenvk::launch_ppo_apply(params, exp_avg, exp_avg_sq, step, grad, obs_dim, *hp,
+                                     as_stream(stream)));
     return FENV_OK;
 }
 

@@ -122,6 +122,16 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
                              const float *old_log_prob, const float *adv, const float *ret,
                              int64_t n, const int64_t *perm, int32_t n_epochs,
                              int32_t batch_size, const ppo_hparams &hp, double *stats,
-                             hipStream_t st);
+                             void *workspace, hipStream_t st);
+size_t ppo_workspace_bytes_impl();
+hipError_t launch_ppo_grad(const float *params, int32_t D, const float *obs, const float *act,
+                           const float *old_log_prob, const float *adv, const float *ret,
+                           const int64_t *rows, int32_t b_local, int32_t b_global,
+                           float adv_mean, float adv_std, int32_t adv_normalize,
+                           int32_t entropy_term, const ppo_hparams &hp, float *grad,
+                           double *stats, hipStream_t st);
+hipError_t launch_ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, float *step,
+                            const float *grad, int32_t D, const ppo_hparams &hp,
+                            hipStream_t st);
 
 }  // namespace fenvk

@@ -29,6 +29,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #ifndef FENV_POLICY_PRIO
 #define FENV_POLICY_PRIO 1
 #endif
@@ -236,20 +238,24 @@ static hipError_t policy_rollout_dm(const Consts &c, const DevState &s, const De
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
     int64_t blocks = (waves + kPRWaves - 1) / kPRWaves;
     if (FENV_PR_PERSISTENT) {
-        static int resident = 0;  // per template instance (D, MODE)
+        // resident workgroups, per template instance (D, MODE) and device (devices may differ)
+        static std::atomic<int> resident_by_dev[64];
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        int resident = (dev >= 0 && dev < 64) ? resident_by_dev[dev].load() : 0;
         if (resident == 0) {
-            int per_cu = 0, dev = 0, cus = 0;
+            int per_cu = 0, cus = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_policy_rollout<D, MODE>,
                                                              64 * kPRWaves, kPRLdsBytes) !=
                     hipSuccess ||
                 per_cu < 1)
                 per_cu = 1;
-            (void)hipGetDevice(&dev);
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                     hipSuccess ||
                 cus < 1)
                 cus = 256;
             resident = per_cu * cus;
+            if (dev >= 0 && dev < 64) resident_by_dev[dev].store(resident);
         }
         if (blocks > resident) blocks = resident;
     }

@@ -39,6 +39,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "fenv.h"
 #include "fenv_internal.h"
 #include "policy_device.h"
@@ -86,6 +90,13 @@ struct PPOArgs {
     ppo_hparams hp;
     double *stats;
     uint64_t *xch;  // split launch: the two blocks' {minibatch + 1, partial grad norm^2} words
+                    // (the caller's workspace: one set per PPO instance, not per device)
+    // gradient mode (ppo_grad, data-parallel update): one minibatch of this rank's rows, loss
+    // means over the GLOBAL minibatch of b_global samples, advantages normalised with the global
+    // minibatch's mean / std; the gradient goes to grad[P] instead of clip + Adam
+    float *grad;
+    float inv_bg, adv_mean, adv_std;
+    int32_t adv_norm_on, ent_once;
 };
 
 // Split launch (FENV_PPO_SPLIT): the actor and the critic each on their own CU.  The two networks'
@@ -202,8 +213,9 @@ __device__ __forceinline__ float wsum(float v) {
 #define FENV_PPO_PHASE(i)
 #endif
 
-template <bool SPLIT>
+template <bool SPLIT, bool GRAD = false>
 __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
+    static_assert(!GRAD || SPLIT, "gradient mode is built on the split (two-CU) layout");
     constexpr int NT = SPLIT ? kPTS : kPT;     // threads of a working block
     constexpr int KP = SPLIT ? kPerTS : kPerT;  // Adam slots per thread
     if (SPLIT && (blockIdx.x & 7) != 0) return;  // split: blocks 0 and 8 work (one XCD)
@@ -246,10 +258,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
         const int p = own(q);
-        m[q] = p < P ? g.exp_avg[p] : 0.0f;
-        v[q] = p < P ? g.exp_avg_sq[p] : 0.0f;
+        m[q] = (!GRAD && p < P) ? g.exp_avg[p] : 0.0f;
+        v[q] = (!GRAD && p < P) ? g.exp_avg_sq[p] : 0.0f;
     }
-    float step = g.step[0];
+    float step = GRAD ? 0.0f : g.step[0];
     // split: the LDS index of each Adam slot's parameter, fixed for the launch; a slot without a
     // parameter points at the pad float after parameter 63 (lx leaves one after every 64; no
     // read ever uses it), so the Adam loop runs branch-free
@@ -318,6 +330,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     // l's advantage a).  It depends on the data only, so the split launch's actor block does it
     // one minibatch ahead, while its norm exchange waits on L2 (adv_nx: wave 0's lanes).
     auto adv_norm = [&](int Bk, float a) -> float {
+        if constexpr (GRAD)  // the global minibatch's statistics, computed by the caller
+            return g.adv_norm_on ? (a - g.adv_mean) / (g.adv_std + 1e-8f) : a;
         if (!(hp.normalize_advantage && Bk > 1)) return a;
         const float invBk = 1.0f / (float)Bk;
         const float x = lane < Bk ? a : 0.0f;
@@ -332,7 +346,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     for (int ep = 0; ep < g.n_epochs; ++ep) {
         for (int64_t s0 = 0; s0 < n; s0 += bs, ++kmb) {
             const int B = (int)((n - s0) < bs ? (n - s0) : bs);
-            const float invB = 1.0f / (float)B;
+            // loss means: over this minibatch, or (gradient mode) over the global minibatch
+            const float invB = GRAD ? g.inv_bg : 1.0f / (float)B;
             float gss = 0.f;  // sum of squares of the gradient entries this thread writes
             // ---- gather the minibatch (from the prefetch registers), then start the next one
 #pragma unroll
@@ -516,11 +531,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         const float kHalfLog2PiE = 1.41893853320467274f;  // 0.5 + 0.5 log(2 pi)
                         const float ent = (kHalfLog2PiE + lsd0) + (kHalfLog2PiE + lsd1);
                         st_pl += (double)(-pl * invB);
-                        st_el += (double)(-ent);
+                        if (!GRAD || g.ent_once) st_el += (double)(-ent);
                         st_cf += (double)(cf * invB);
                         // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef (d log(exp(ls))/d ls
                         // = 1)
-                        const float g0 = gls0 - hp.ent_coef, g1 = gls1 - hp.ent_coef;
+                        // gradient mode: the entropy term once over the ranks (ent_once)
+                        const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
+                        const float g0 = gls0 - ec, g1 = gls1 - ec;
                         G[lx(L.logstd)] = g0;
                         G[lx(L.logstd + 1)] = g1;
                         G[lx(L.actb)] = sgmu0;
@@ -745,6 +762,15 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
                 gss = __builtin_fmaf(acc, acc, gss);
             }
+            if constexpr (GRAD) {  // this rank's share of the minibatch gradient, unclipped
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < KP; ++q) {
+                    const int p = own(q);
+                    if (p < P) g.grad[p] = G[lx(p)];
+                }
+                continue;
+            }
             // ---- clip_grad_norm_(max_grad_norm): global 2-norm from the squares each thread
             // accumulated as it wrote its gradient entries (every entry is written exactly once
             // per minibatch), one wave sum each, reduced after the barrier
@@ -837,12 +863,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
         const int p = own(q);
-        if (p < P) g.params[p] = W[lx(p)];
+        if (!GRAD && p < P) g.params[p] = W[lx(p)];
     }
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
         const int p = own(q);
-        if (p < P) {
+        if (!GRAD && p < P) {
 #if FENV_PPO_DUMP_GRAD  // diagnostic build: the last minibatch's unclipped gradient, its
                         // observations and dL/dz1 rows
             g.exp_avg[p] = G[lx(p)];
@@ -855,7 +881,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         }
     }
     if (tid == 0 && net_b == 0) {
-        g.step[0] = step;
+        if (!GRAD) g.step[0] = step;
         atomicAdd(g.stats + 0, st_pl);  // atomic: the other block may mark a lost exchange
         if (!SPLIT) g.stats[1] += st_vl;
         g.stats[2] += st_el;
@@ -876,48 +902,131 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     }
 }
 
+// clip_grad_norm_ + Adam over the (all-reduced) gradient of a data-parallel minibatch
+// (ppo_apply): torch semantics, in torch's capturable-Adam operation order
+// (torch/optim/adam.py _single_tensor_adam, capturable branch).  One workgroup: the 2-norm is
+// summed in a fixed order (thread k: elements k, k + NT, ...; then a fixed tree).
+constexpr int kAT = 1024;
+__global__ __launch_bounds__(kAT) void k_ppo_apply(float *params, float *exp_avg,
+                                                   float *exp_avg_sq, float *step,
+                                                   const float *grad, int P, ppo_hparams hp) {
+    __shared__ float red[kAT / 64];
+    __shared__ float s_coef, s_step;
+    const int tid = threadIdx.x;
+    float ss = 0.f;
+    for (int p = tid; p < P; p += kAT) ss = __builtin_fmaf(grad[p], grad[p], ss);
+    ss = wsum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    if (tid == 0) {
+        float tot = 0.f;
+        for (int k = 0; k < kAT / 64; ++k) tot += red[k];
+        const float norm = __builtin_sqrtf(tot);
+        const float c = hp.max_grad_norm / (norm + 1e-6f);
+        s_coef = c < 1.0f ? c : 1.0f;
+        s_step = step[0] + 1.0f;
+        step[0] = s_step;
+    }
+    __syncthreads();
+    const float coef = s_coef, st = s_step;
+    const float bc1 = 1.0f - powf(hp.beta1, st), bc2 = 1.0f - powf(hp.beta2, st);
+    const float step_size = hp.lr / bc1, ssn = -step_size;
+    const float bc2s = __builtin_sqrtf(bc2);
+    for (int p = tid; p < P; p += kAT) {
+        const float gr = grad[p] * coef;
+        const float m = exp_avg[p] + (1.0f - hp.beta1) * (gr - exp_avg[p]);  // lerp_, weight < 0.5
+        const float v = exp_avg_sq[p] * hp.beta2 + (1.0f - hp.beta2) * gr * gr;  // mul_ + addcmul_
+        exp_avg[p] = m;
+        exp_avg_sq[p] = v;
+        const float denom = __builtin_sqrtf(v) / (bc2s * ssn) + hp.eps / ssn;
+        params[p] = params[p] + m / denom;  // addcdiv_
+    }
+}
+
+static hipError_t ppo_smem_attr(const void *fn) {
+    // once per (kernel, device): hipFuncSetAttribute is device-scoped
+    static std::mutex mu;
+    static std::set<std::pair<const void *, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({fn, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPPOLdsBytes);
+    if (e == hipSuccess) done.insert({fn, dev});
+    return e;
+}
+
+static bool split_fits(int32_t D) {
+    const PLayout L(D);
+    return (L.vf0W - L.pi0W) + (L.valW - L.actW) + 2 <= kPTS * kPerTS &&
+           (L.actW - L.vf0W) + (L.logstd - L.valW) <= kPTS * kPerTS;
+}
+
+size_t ppo_workspace_bytes_impl() { return 4 * sizeof(uint64_t); }
+
 hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
                              int32_t D, const float *obs, const float *act,
                              const float *old_log_prob, const float *adv, const float *ret,
                              int64_t n, const int64_t *perm, int32_t n_epochs,
                              int32_t batch_size, const ppo_hparams &hp, double *stats,
-                             hipStream_t st) {
+                             void *workspace, hipStream_t st) {
     constexpr bool split = FENV_PPO_SPLIT != 0;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_ppo_update<split>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kPPOLdsBytes);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    hipError_t e = ppo_smem_attr(reinterpret_cast<const void *>(&k_ppo_update<split>));
+    if (e != hipSuccess) return e;
     uint64_t *xch = nullptr;
+    bool own_ws = false;
     if (split) {
-        // exchange words, two per block and device, cleared before every launch (sequence
-        // numbers restart at 1)
-        static uint64_t *words[64] = {};  // 32 B per device, kept for the process lifetime
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-        if (!words[dev]) {
-            e = hipMalloc(&words[dev], 4 * sizeof(uint64_t));
+        if (!split_fits(D)) return hipErrorInvalidValue;
+        // the exchange words: the caller's workspace (one per PPO instance), or, without one, a
+        // stream-ordered allocation for this launch only -- never shared between launches that
+        // may run concurrently.  Cleared on the launch's stream (sequence numbers restart at 1).
+        xch = static_cast<uint64_t *>(workspace);
+        if (!xch) {
+            e = hipMallocAsync(reinterpret_cast<void **>(&xch), ppo_workspace_bytes_impl(), st);
             if (e != hipSuccess) return e;
+            own_ws = true;
         }
-        xch = words[dev];
-        e = hipMemsetAsync(xch, 0, 4 * sizeof(uint64_t), st);
+        e = hipMemsetAsync(xch, 0, ppo_workspace_bytes_impl(), st);
         if (e != hipSuccess) return e;
-        const PLayout L(D);
-        if ((L.vf0W - L.pi0W) + (L.valW - L.actW) + 2 > kPTS * kPerTS ||
-            (L.actW - L.vf0W) + (L.logstd - L.valW) > kPTS * kPerTS)
-            return hipErrorInvalidValue;
     }
     PPOArgs g{params, exp_avg, exp_avg_sq, step, obs, act, old_log_prob, adv, ret, perm, n,
-              D, n_epochs, batch_size, hp, stats, xch};
+              D, n_epochs, batch_size, hp, stats, xch, nullptr, 0.f, 0.f, 1.f, 0, 1};
     if (split)
         hipLaunchKernelGGL(k_ppo_update<true>, dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
     else
         hipLaunchKernelGGL(k_ppo_update<false>, dim3(1), dim3(kPT), kPPOLdsBytes, st, g);
+    e = hipGetLastError();
+    if (own_ws) {
+        const hipError_t ef = hipFreeAsync(xch, st);
+        if (e == hipSuccess) e = ef;
+    }
+    return e;
+}
+
+hipError_t launch_ppo_grad(const float *params, int32_t D, const float *obs, const float *act,
+                           const float *old_log_prob, const float *adv, const float *ret,
+                           const int64_t *rows, int32_t b_local, int32_t b_global,
+                           float adv_mean, float adv_std, int32_t adv_normalize,
+                           int32_t entropy_term, const ppo_hparams &hp, float *grad,
+                           double *stats, hipStream_t st) {
+    if (!split_fits(D)) return hipErrorInvalidValue;
+    hipError_t e = ppo_smem_attr(reinterpret_cast<const void *>(&k_ppo_update<true, true>));
+    if (e != hipSuccess) return e;
+    PPOArgs g{const_cast<float *>(params), nullptr, nullptr, nullptr, obs, act, old_log_prob,
+              adv, ret, rows, (int64_t)b_local, D, 1, b_local, hp, stats, nullptr, grad,
+              1.0f / (float)b_global, adv_mean, adv_std,
+              (adv_normalize && b_global > 1) ? 1 : 0, entropy_term ? 1 : 0};
+    hipLaunchKernelGGL((k_ppo_update<true, true>), dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, float *step,
+                            const float *grad, int32_t D, const ppo_hparams &hp,
+                            hipStream_t st) {
+    const PLayout L(D);
+    hipLaunchKernelGGL(k_ppo_apply, dim3(1), dim3(kAT), 0, st, params, exp_avg, exp_avg_sq, step,
+                       grad, L.total, hp);
     return hipGetLastError();
 }
 

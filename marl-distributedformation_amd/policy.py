@@ -40,6 +40,11 @@ def _shape(shp, D):
     return tuple(D if s == "D" else s for s in shp)
 
 
+def param_shapes(obs_dim: int):
+    """[(SB3 name, shape)] in flat-buffer order for observation size ``obs_dim`` (no device)."""
+    return [(k, _shape(shp, obs_dim)) for k, shp in PARAM_SPECS]
+
+
 class MlpPolicy:
     """Flat-parameter actor-critic with SB3 naming; forward on the HIP kernel."""
 

@@ -27,7 +27,8 @@ import torch.nn.functional as Fn
 
 from . import checkpoint as ckpt
 from . import distributed as pdist
-from .policy import MlpPolicy
+from .dp_update import ShardedUpdate
+from .policy import MlpPolicy, param_shapes
 from .rollout import RolloutBuffer, RolloutCollector
 
 _CAPTURE_STREAMS: dict = {}
@@ -56,15 +57,20 @@ class PPOConfig:
     vf_coef: float = 0.5
     max_grad_norm: float = 0.5
     normalize_advantage: bool = True
+    # several ranks: "replicated" = one all-gather of every rank's samples per update, then the
+    # same sequential update on every rank (SB3's exact minibatches); "sharded" = each rank keeps
+    # its samples and takes batch_size / world rows of every global minibatch, with one gradient
+    # all-reduce per minibatch (dp_update.py)
+    update_mode: str = "replicated"
 
 
-def evaluate_actions(policy: MlpPolicy, flat: torch.Tensor, obs: torch.Tensor,
-                     actions: torch.Tensor):
-    """SB3 ActorCriticPolicy.evaluate_actions as differentiable torch ops on views of `flat`."""
-    D = policy.obs_dim
+def evaluate_actions(policy, flat: torch.Tensor, obs: torch.Tensor, actions: torch.Tensor):
+    """SB3 ActorCriticPolicy.evaluate_actions as differentiable torch ops on views of `flat`.
+    ``policy``: an :class:`MlpPolicy`, or the observation size (int) alone."""
+    shapes = param_shapes(policy) if isinstance(policy, int) else policy.param_shapes()
     o = 0
     P = {}
-    for k, shp in policy.param_shapes():
+    for k, shp in shapes:
         n = math.prod(shp)
         P[k] = flat[o:o + n].view(shp)
         o += n
@@ -84,7 +90,6 @@ def evaluate_actions(policy: MlpPolicy, flat: torch.Tensor, obs: torch.Tensor,
     log_prob = (-((actions - mu) ** 2) / (2 * var) - std.log()
                 - math.log(math.sqrt(2 * math.pi))).sum(-1)
     entropy = (0.5 + 0.5 * math.log(2 * math.pi) + std.log()).sum(-1)
-    del D
     return values, log_prob, entropy
 
 
@@ -115,19 +120,24 @@ class PPO:
         self.collector = RolloutCollector(env, self.policy, self.buffer, seed=seed)
         N = env.num_agents_per_formation
         self.total_envs = env.num_envs
+        self.counts = [env.num_envs]
         if self.world > 1:  # the env is this rank's shard of total_formations
             self.total_envs = int(env.total_formations) * N
             self.counts = pdist.shard_counts(int(env.total_formations), self.world, N)
             if self.counts[self.rank] != env.num_envs:
                 raise ValueError("env shard does not match distributed.shard_range(total_formations, "
                                  "rank, world)")
+        if self.cfg.update_mode not in ("replicated", "sharded"):
+            raise ValueError("update_mode must be 'replicated' or 'sharded'")
+        self.sharded = self.cfg.update_mode == "sharded"
         T, D = self.cfg.n_steps, env.obs_dim
         # update samples [T, A_total, D + 5] = obs | action(2) | log_prob | advantage | return;
-        # with one rank they are views of the rollout buffer instead
+        # with one rank (or the sharded update) they are views of the rollout buffer instead
+        rep_gather = self.world > 1 and not self.sharded
         self._gsamples = (torch.empty((T, self.total_envs, D + 5), dtype=torch.float32,
-                                      device=env.device) if self.world > 1 else None)
+                                      device=env.device) if rep_gather else None)
         self._lsamples = (torch.empty((T, env.num_envs, D + 5), dtype=torch.float32,
-                                      device=env.device) if self.world > 1 else None)
+                                      device=env.device) if rep_gather else None)
         self.param = torch.nn.Parameter(self.policy.flat)  # shares storage with the kernel's
         self.param.grad = torch.zeros_like(self.param)     # static: graph replays write it
         # capturable: the step count lives on the device, so the update can be graph-captured
@@ -147,6 +157,12 @@ class PPO:
         # batch_size <= 64 (SB3's default 64): the whole update as one HIP kernel (ppo_update)
         self.use_fused = ((self.param.device.type == "cuda" and self.cfg.batch_size <= 64)
                           if use_fused is None else use_fused)
+        # the fused update's exchange words: this instance's own (include/fenv.h ppo_update_ws)
+        from . import _lib
+        self._ws = (torch.zeros(int(_lib.lib().ppo_workspace_bytes()), dtype=torch.uint8,
+                                device=dev) if self.param.device.type == "cuda" else None)
+        self._dp = (ShardedUpdate(self.cfg, D, [T * c for c in self.counts], seed, dev,
+                                  fused=self.use_fused) if self.sharded else None)
 
     @property
     def num_timesteps(self) -> int:
@@ -156,7 +172,7 @@ class PPO:
     # ---------------------------------------------------------------- samples
     def gather_samples(self) -> None:
         """World > 1: assemble the global update buffer (one all-gather, unsharded order)."""
-        if self.world == 1:
+        if self.world == 1 or self.sharded:
             return
         b, D = self.buffer, self.buffer.obs_dim
         ls = self._lsamples
@@ -170,7 +186,7 @@ class PPO:
     def _flat(self):
         """(obs, actions, old_log_prob, advantages, returns) over the update's n samples."""
         b, D = self.buffer, self.buffer.obs_dim
-        if self.world == 1:
+        if self.world == 1 or self.sharded:
             n = b.n_steps * b.n_envs
             return (b.observations.reshape(n, D), b.actions.reshape(n, 2),
                     b.log_probs.reshape(n), b.advantages.reshape(n), b.returns.reshape(n))
@@ -270,19 +286,29 @@ class PPO:
         steps = c.n_epochs * (-(-n // bs))
         for attempt in range(2):
             self._sums.zero_()
-            _lib.check(_lib.lib().ppo_update(
+            _lib.check(_lib.lib().ppo_update_ws(
                 _lib.ptr(self.param), _lib.ptr(st["exp_avg"]), _lib.ptr(st["exp_avg_sq"]),
                 _lib.ptr(st["step"]), self.buffer.obs_dim, _lib.ptr(obs), _lib.ptr(act),
                 _lib.ptr(lp), _lib.ptr(adv), _lib.ptr(ret), n, _lib.ptr(perm), c.n_epochs, bs,
-                ctypes.byref(hp), _lib.ptr(self._sums), _lib.current_stream(dev)), "ppo_update")
+                ctypes.byref(hp), _lib.ptr(self._sums), _lib.ptr(self._ws),
+                _lib.current_stream(dev)), "ppo_update_ws")
             m = (self._sums / steps).tolist()
-            if not (math.isnan(m[0]) and m[3] < 0):
+            lost = math.isnan(m[0]) and m[3] < 0
+            # the ranks decide together: a retry (or the raise below) on one rank only would leave
+            # the others blocked in the next collective
+            if self.world > 1:
+                lost = pdist.max_over_ranks(1.0 if lost else 0.0, dev) > 0
+            if not lost:
                 break
-            # the two workgroups' norm exchange timed out (include/fenv.h): restore, run again
+            # a norm exchange timed out (include/fenv.h): every rank restores and runs again
             self.exchange_retries += 1
             with torch.no_grad():
                 for t, s in zip(state, snap):
                     t.copy_(s)
+        if self.world > 1:  # any rank's NaN makes every rank raise
+            bad = pdist.max_over_ranks(1.0 if math.isnan(m[0]) else 0.0, dev) > 0
+            if bad and not math.isnan(m[0]):
+                raise RuntimeError("fused PPO update failed on another rank")
         if math.isnan(m[0]):
             raise RuntimeError("fused PPO update: NaN policy loss (" +
                                ("the two-CU launch's gradient-norm exchange timed out twice)"
@@ -297,6 +323,9 @@ class PPO:
         buffer, identically on every rank.  Full minibatches replay the captured graph; a
         trailing partial minibatch runs eagerly.  Losses are summed on the device and read once
         at the end."""
+        if self.sharded:
+            self.stats = self._dp.run(self.param, self.opt, self._flat())
+            return self.stats
         self.gather_samples()
         if self.use_fused and self.cfg.batch_size <= 64:
             return self._train_fused()

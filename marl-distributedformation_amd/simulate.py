@@ -4,11 +4,18 @@ The reference keeps one ``FormationSimulator`` object per formation (simulate.py
 exposes them as ``FormationEnv.formationsim_list`` (vectorized_env.py:38-43); its consumers read
 ``agents``, ``goal``, ``steps_since_reset`` and, for formation 0 in playback, the matplotlib
 ``fig`` (visualize_policy.py:38,43).  Here the state of every formation lives in HBM inside one
-libfenv handle, so ``formationsim_list`` is a lazy sequence of read-only views that copy one
-formation's slice to the host on access.  The simulation itself never runs through them.
+libfenv handle, so ``formationsim_list`` is a lazy sequence of read-only views.  A view reads
+only its own formation: ``fenv_get_state_range`` copies its N agents' slice and
+``fenv_metrics_range`` scores only that formation, so one access costs O(N), whatever the env's
+size.  The simulation itself never runs through them.
+
+Views hold the env through a weak reference: an env and its views form no reference cycle, so a
+dropped env is freed by reference counting at a known point rather than by the cyclic garbage
+collector at an arbitrary one.
 """
 from __future__ import annotations
 
+import weakref
 from collections.abc import Sequence
 
 import numpy as np
@@ -26,7 +33,7 @@ class FormationView:
     num_obstacles = 0
 
     def __init__(self, env, index: int):
-        self._env = env
+        self._envref = weakref.ref(env)
         self.index = int(index)
         self.num_agents = env.num_agents_per_formation
         self.goal_in_obs = env.goal_in_obs
@@ -34,6 +41,13 @@ class FormationView:
         self.desired_neighbor_dist = float(env.desired_neighbor_dist)
         self.visualize = False
         self.log = False
+
+    @property
+    def _env(self):
+        env = self._envref()
+        if env is None:
+            raise ReferenceError("the FormationEnv of this view no longer exists")
+        return env
 
     # -- state (simulate.py:133 agents [N,2], :140 goal [2], :147 steps_since_reset)
     def _slice(self):
@@ -59,19 +73,23 @@ class FormationView:
 
     def compute_obs(self) -> torch.Tensor:
         """Observation rows of this formation (simulate.py:150-174)."""
-        obs = self._env.observe_tensor()
+        env = self._env
+        obs = env.observe_tensor()
         N = self.num_agents
         return obs[self.index * N:(self.index + 1) * N].cpu()
 
+    def _metrics(self) -> list:
+        return self._env.metrics_range(self.index, 1)[0].tolist()
+
     def compute_metrics(self) -> dict:
         """simulate.py:238-254 (the values the reference logs when ``log``)."""
-        m = self._env.metrics()[self.index].tolist()
+        m = self._metrics()
         return {"avg_dist_to_goal": m[0], "ave_dist_to_neighbor": m[1],
                 "std_dist_to_neighbor": m[2]}
 
     def reward_components(self) -> dict:
         """The means compute_reward_and_done logs (simulate.py:183-208) for the last step."""
-        m = self._env.metrics()[self.index].tolist()
+        m = self._metrics()
         return dict(zip(("close_to_goal_reward", "reward_dist", "reward_right_neighbor",
                          "reward_left_neighbor"), m[4:8]))
 
@@ -83,7 +101,7 @@ class FormationViewList(Sequence):
     """Lazy ``formationsim_list``: view objects are created on first access and cached."""
 
     def __init__(self, env, count: int):
-        self._env = env
+        self._envref = weakref.ref(env)
         self._n = int(count)
         self._cache: dict[int, FormationView] = {}
 
@@ -100,5 +118,8 @@ class FormationViewList(Sequence):
             raise IndexError("formation index out of range")
         v = self._cache.get(i)
         if v is None:
-            v = self._cache[i] = self._env._make_view(i)
+            env = self._envref()
+            if env is None:
+                raise ReferenceError("the FormationEnv of this list no longer exists")
+            v = self._cache[i] = env._make_view(i)
         return v

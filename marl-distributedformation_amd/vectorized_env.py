@@ -139,6 +139,7 @@ class FormationEnv(_BASE):
             _lib.lib().fenv_desired_neighbor_dist(self.num_agents_per_formation))
 
         L = _lib.lib()
+        _lib.flush_deferred()
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(L.fenv_create(ctypes.byref(h), self.device.index, self.num_formation,
@@ -168,14 +169,45 @@ class FormationEnv(_BASE):
     def _stream(self):
         return _lib.current_stream(self.device)
 
+    def release(self) -> None:
+        """Free this env's device state, its staging buffers and its host mirrors now.
+
+        Idempotent.  Afterwards every device call raises.  The reference has no such path: its
+        ``close()`` raises NotImplementedError (vectorized_env.py:87-88), which is kept, so this
+        is the deterministic teardown (also ``with FormationEnv(cfg) as env: ...``).  Without it
+        the env is freed when its last reference goes (views hold only weak references), or --
+        for a handle dropped while a HIP graph is being captured -- at the next create/release
+        (``_lib.destroy_handle``)."""
+        h = getattr(self, "_h", None)
+        self._h = None
+        if h is not None and h.value:
+            # finish the work this env queued on the caller's stream before its buffers go
+            torch.cuda.current_stream(self.device).synchronize()
+            _lib.destroy_handle(h)
+        self._host = None
+        for k in ("obs_dev", "rew_dev", "done_dev", "_act_dev"):
+            if hasattr(self, k):
+                setattr(self, k, None)
+
+    @property
+    def released(self) -> bool:
+        return getattr(self, "_h", None) is None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()
+        return False
+
     def __del__(self):
         h = getattr(self, "_h", None)
+        self._h = None
         if h is not None and h.value:
             try:
-                _lib.lib().fenv_destroy(h)
+                _lib.destroy_handle(h)
             except Exception:
                 pass
-            self._h = None
 
     def _ensure_host(self):
         if self._host is None:
@@ -198,11 +230,10 @@ class FormationEnv(_BASE):
         return v
 
     def _formation_state(self, i: int):
-        N = self.num_agents_per_formation
-        px, py, gx, gy, t = self.get_state()
-        sl = slice(i * N, (i + 1) * N)
-        return (px[sl].cpu().numpy(), py[sl].cpu().numpy(), float(gx[i]), float(gy[i]),
-                int(t[i]))
+        """Formation i's state on the host, copying only its N agents (fenv_get_state_range)."""
+        px, py, gx, gy, t = self.get_state_range(i, 1)
+        px, py, gx, gy, t = (v.cpu().numpy() for v in (px, py, gx, gy, t))
+        return px, py, float(gx[0]), float(gy[0]), int(t[0])
 
     def _refresh_fig(self):
         if self._fig is None:
@@ -473,6 +504,39 @@ class FormationEnv(_BASE):
         _lib.check(_lib.lib().fenv_get_state(self._h, *(_lib.ptr(v) for v in (px, py, gx, gy, t)),
                                              self._stream()), "fenv_get_state")
         return px, py, gx, gy, t
+
+    def _check_range(self, first: int, count: int) -> tuple:
+        first, count = int(first), int(count)
+        if count < 1 or first < 0 or first + count > self.num_formation:
+            raise IndexError(f"formations [{first}, {first + count}) outside [0, "
+                             f"{self.num_formation})")
+        return first, count
+
+    def get_state_range(self, first: int, count: int):
+        """State of formations [first, first + count) only (``fenv_get_state_range``):
+        (px [count*N], py [count*N], gx [count], gy [count], t [count]) device tensors."""
+        first, count = self._check_range(first, count)
+        n, dev = count * self.num_agents_per_formation, self.device
+        px = torch.empty(n, dtype=torch.float32, device=dev)
+        py = torch.empty(n, dtype=torch.float32, device=dev)
+        gx = torch.empty(count, dtype=torch.float32, device=dev)
+        gy = torch.empty(count, dtype=torch.float32, device=dev)
+        t = torch.empty(count, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().fenv_get_state_range(
+            self._h, first, count, *(_lib.ptr(v) for v in (px, py, gx, gy, t)), self._stream()),
+            "fenv_get_state_range")
+        return px, py, gx, gy, t
+
+    def metrics_range(self, first: int, count: int, rew: torch.Tensor | None = None):
+        """:meth:`metrics` of formations [first, first + count) only (``fenv_metrics_range``):
+        [count, 8]; ``rew`` (optional) holds those formations' count*N rewards."""
+        first, count = self._check_range(first, count)
+        self._check_out("rew", rew, (count * self.num_agents_per_formation,), torch.float32)
+        out = torch.empty((count, 8), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().fenv_metrics_range(self._h, first, count, _lib.ptr(rew),
+                                                 _lib.ptr(out), None, self._stream()),
+                   "fenv_metrics_range")
+        return out
 
     def set_state(self, px, py, gx, gy, t) -> None:
         dev = self.device

@@ -208,3 +208,22 @@ def test_formation_size_limits(pkg):
     for N in (0, (1 << 24) + 1):
         with pytest.raises(ValueError):
             cfgm.validate(cfgm.as_config({"num_formation": 2, "num_agents_per_formation": N}))
+
+
+def test_abi_version_matches_header(flib):
+    """fenv_abi_version() == the header's FENV_ABI_VERSION (a host program checks this at start)."""
+    import re
+    src = open(flib.HEADER).read()
+    want = int(re.search(r"#define FENV_ABI_VERSION (\d+)", src).group(1))
+    assert flib.lib().fenv_abi_version() == want >= 2
+    assert flib.lib().ppo_workspace_bytes() >= 16
+
+
+def test_destroy_null_and_range_args_fail_cleanly(flib):
+    """fenv_destroy(NULL) is a no-op; the range queries reject a NULL handle with an error code
+    (no device needed)."""
+    L = flib.lib()
+    assert L.fenv_destroy(None) == 0
+    assert L.fenv_get_state_range(None, 0, 1, None, None, None, None, None, None) != 0
+    assert L.fenv_metrics_range(None, 0, 1, None, None, None, None) != 0
+    assert b"NULL" in L.fenv_last_error()

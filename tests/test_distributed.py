@@ -129,3 +129,145 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     ppo = import_module(pkgload.load().__name__ + ".ppo")
     perms = ppo.epoch_permutations(3 * total * N, 4, torch.Generator().manual_seed(7), "cpu")
     assert got[0][1] == got[1][1] == perms.numpy().tobytes()
+
+
+# ------------------------------------------------------------------ data-parallel PPO update
+_DP = dict(D=8, n=(18, 13), epochs=3, batch=8, seed=5)
+
+
+def _dp_samples(rank):
+    """Rank r's local update samples (obs, actions, old_log_prob, advantages, returns)."""
+    g = torch.Generator().manual_seed(1000 + rank)
+    n, D = _DP["n"][rank], _DP["D"]
+    obs = torch.rand((n, D), generator=g) * 2 - 1
+    act = torch.randn((n, 2), generator=g) * 0.7
+    lp = -torch.rand(n, generator=g) * 3 - 1
+    adv = torch.randn(n, generator=g) * 2
+    ret = torch.randn(n, generator=g)
+    return obs, act, lp, adv, ret
+
+
+def _dp_init_params():
+    from importlib import import_module
+    import pkgload
+    pol = import_module(pkgload.load().__name__ + ".policy")
+    n = sum(int(np.prod(s)) for _, s in pol.param_shapes(_DP["D"]))
+    g = torch.Generator().manual_seed(3)
+    flat = torch.randn(n, generator=g) * 0.2
+    flat[-2:] = torch.tensor([-0.3, 0.1])  # log_std
+    return flat
+
+
+def _dp_cfg():
+    from importlib import import_module
+    import pkgload
+    ppo = import_module(pkgload.load().__name__ + ".ppo")
+    return ppo.PPOConfig(n_epochs=_DP["epochs"], batch_size=_DP["batch"], update_mode="sharded")
+
+
+def _dp_worker(rank, world, port, root, q):
+    import sys
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import pkgload
+    pkg = pkgload.load()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".distributed")
+    dpu = import_module(pkg.__name__ + ".dp_update")
+    d.init_from_env(backend="gloo")
+    param = torch.nn.Parameter(_dp_init_params())
+    opt = torch.optim.Adam([param], lr=1e-3, eps=1e-5)
+    upd = dpu.ShardedUpdate(_dp_cfg(), _DP["D"], list(_DP["n"]), _DP["seed"], "cpu")
+    stats = upd.run(param, opt, _dp_samples(rank))
+    st = opt.state[param]
+    got = [None] * world
+    dist.all_gather_object(got, (param.detach().numpy().tobytes(),
+                                 st["exp_avg_sq"].numpy().tobytes(), stats))
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_update_equals_concatenated_minibatches():
+    """The data-parallel update (dp_update.py: each rank takes batch_size / world rows of every
+    global minibatch, one gradient all-reduce per minibatch) on 2 ranks with uneven shards (18 +
+    13 samples: the last minibatch has rows on rank 0 only) equals the single-process SB3 update
+    whose minibatches are the concatenations of the ranks' rows -- to summation order."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] == got[1][0] and got[0][1] == got[1][1]  # replicated state, bit for bit
+    # single-process reference: SB3 PPO.train over the concatenated minibatches
+    import math
+    from importlib import import_module
+    import pkgload
+    pkg = pkgload.load()
+    ppo = import_module(pkg.__name__ + ".ppo")
+    dpu = import_module(pkg.__name__ + ".dp_update")
+    cfg = _dp_cfg()
+    b, M, rows, _ = dpu.minibatch_plan(list(_DP["n"]), cfg.batch_size, 2)
+    assert rows[1][-1] == 0 and M == 5
+    perms = []
+    for r in range(2):
+        gen = torch.Generator().manual_seed((_DP["seed"] * 1_000_003 + r) & 0x7FFFFFFFFFFFFFFF)
+        perms.append([torch.randperm(_DP["n"][r], generator=gen) for _ in range(cfg.n_epochs)])
+    local = [_dp_samples(r) for r in range(2)]
+    param = torch.nn.Parameter(_dp_init_params())
+    opt = torch.optim.Adam([param], lr=1e-3, eps=1e-5)
+    sums = torch.zeros(4, dtype=torch.float64)
+    for e in range(cfg.n_epochs):
+        for j in range(M):
+            parts = [tuple(t[perms[r][e][j * b:j * b + rows[r][j]]] for t in local[r])
+                     for r in range(2)]
+            obs, act, old_lp, adv, ret = (torch.cat([p[k] for p in parts]) for k in range(5))
+            values, log_prob, entropy = ppo.evaluate_actions(_DP["D"], param, obs, act)
+            if adv.numel() > 1:
+                adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+            ratio = torch.exp(log_prob - old_lp)
+            l1 = adv * ratio
+            l2 = adv * torch.clamp(ratio, 1 - cfg.clip_range, 1 + cfg.clip_range)
+            pl = -torch.min(l1, l2).mean()
+            vl = torch.nn.functional.mse_loss(ret, values)
+            el = -torch.mean(entropy)
+            loss = pl + cfg.ent_coef * el + cfg.vf_coef * vl
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_([param], cfg.max_grad_norm)
+            opt.step()
+            cf = (torch.abs(ratio - 1) > cfg.clip_range).float().mean()
+            sums += torch.stack([pl.detach(), vl.detach(), el.detach(), cf]).double()
+    want = param.detach()
+    have = torch.from_numpy(np.frombuffer(got[0][0], np.float32).copy())
+    assert (have - want).abs().max().item() < 2e-6, (have - want).abs().max().item()
+    assert not torch.equal(want, _dp_init_params())  # the update moved the parameters
+    ref = (sums / (cfg.n_epochs * M)).tolist()
+    stats = got[0][2]
+    for k, name in enumerate(("policy_gradient_loss", "value_loss", "entropy_loss",
+                              "clip_fraction")):
+        assert math.isclose(stats[name], ref[k], rel_tol=1e-5, abs_tol=1e-6), (name, stats, ref)
+
+
+def test_sharded_minibatch_plan(pkg):
+    """minibatch_plan: every rank runs the same number of minibatches per epoch; the rows of
+    minibatch j over the ranks sum to the global minibatch; batch_size must split evenly."""
+    from importlib import import_module
+    dpu = import_module(pkg.__name__ + ".dp_update")
+    b, M, rows, bg = dpu.minibatch_plan([300, 250], 64, 2)
+    assert (b, M) == (32, 10)
+    assert all(sum(r) == n for r, n in zip(rows, [300, 250]))
+    assert bg == [rows[0][j] + rows[1][j] for j in range(M)] and bg[0] == 64
+    assert rows[1][-2:] == [26, 0] or rows[1][-1] == 0
+    b, M, rows, bg = dpu.minibatch_plan([50000], 64, 1)
+    assert (b, M, bg[-1]) == (64, 782, 16)  # the reference's 1000 x 5 x 10 samples
+    with pytest.raises(ValueError):
+        dpu.minibatch_plan([10, 10], 63, 2)

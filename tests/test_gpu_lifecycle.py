@@ -1,0 +1,171 @@
+"""Env lifecycle on the GPU: deterministic release, teardown from
+the garbage collector and inside a HIP graph capture, and O(N) formation views.
+
+Round 2 saw one SIGABRT during garbage collection.  Envs then formed a reference
+cycle with their formation views, so every dropped env -- its device state, its pinned host
+mirrors, its torch buffers -- was torn down by the cyclic collector at arbitrary points.  These
+tests churn a few hundred envs over every kernel path with explicit collections in between."""
+import gc
+import weakref
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import COracleEnv, synth_actions
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def make_env(venv, F, N, goal=True, seed=0, **kw):
+    cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": goal}
+    return venv.FormationEnv(cfg, device=DEV, seed=seed, **kw)
+
+
+def test_env_has_no_reference_cycle(venv):
+    """A dropped env (views accessed, numpy face used) is freed by reference counting alone."""
+    env = make_env(venv, 7, 5)
+    env.reset()
+    env.step(np.zeros((35, 2), np.float32))
+    v = env.formationsim_list[3]
+    _ = v.agents, v.goal, v.steps_since_reset
+    ref = weakref.ref(env)
+    gc.disable()
+    try:
+        del env
+        assert ref() is None, "FormationEnv survived its last reference: a reference cycle"
+    finally:
+        gc.enable()
+    with pytest.raises(ReferenceError):
+        _ = v.agents
+
+
+def test_release_is_deterministic_and_idempotent(venv, flib):
+    env = make_env(venv, 16, 5)
+    env.reset()
+    base = torch.cuda.memory_allocated()
+    with make_env(venv, 4096, 5) as big:
+        big.reset()
+        big.rollout(torch.zeros((3, big.num_envs, 2), device=DEV))
+        assert torch.cuda.memory_allocated() > base
+    assert big.released
+    assert torch.cuda.memory_allocated() <= base  # the env's torch buffers went with it
+    big.release()  # idempotent
+    with pytest.raises(Exception):
+        big.step_tensor(torch.zeros((big.num_envs, 2), device=DEV))
+    with pytest.raises(NotImplementedError):  # the reference's close() contract is kept
+        env.close()
+    assert flib.lib().fenv_destroy(None) == 0
+    env.release()
+
+
+def test_churn_envs_across_paths_with_gc(venv):
+    """Create and drop ~300 envs over the wavefront (N <= 64, incl. the staged and role-split
+    kernels), workgroup (64 < N <= 1024) and large-formation (N > 1024) paths, both reset modes,
+    the numpy face (pinned host mirrors) and the device faces, some released explicitly, some
+    dropped, some left to the collector, with gc.collect() interleaved; every 25th env is checked
+    against the C oracle bit for bit."""
+    shapes = [(5, 1), (1, 5), (4096, 5), (60, 64), (3, 100), (2, 1024), (2, 1025), (1, 1300),
+              (2500, 5), (7, 33)]
+    rng = np.random.default_rng(0)
+    keep = []
+    checked = 0
+    for i in range(300):
+        F, N = shapes[(i + i // 25) % len(shapes)]
+        mode = "philox" if i % 3 == 1 else "mt19937"
+        env = make_env(venv, F, N, goal=bool(i % 2), seed=i, reset_mode=mode, max_steps=3)
+        A = F * N
+        if i % 25 == 0 and mode == "mt19937":
+            ref = COracleEnv(F, N, bool(i % 2), i, max_steps=3)
+            o = env.reset()
+            assert np.array_equal(o.view(np.uint32), ref.reset().view(np.uint32))
+            for k in range(6):
+                a = synth_actions(i, k, A, 1.2)
+                o, r, d, _ = env.step(a)
+                ro, rr, rd, _ = ref.step(a)
+                assert np.array_equal(o.view(np.uint32), ro.view(np.uint32)), (F, N, k)
+                assert np.array_equal(r.view(np.uint32), rr.view(np.uint32)), (F, N, k)
+                assert np.array_equal(d, rd), (F, N, k)
+            checked += 1
+        elif i % 4 == 0:
+            env.reset()
+            env.step(rng.uniform(-1, 1, (A, 2)).astype(np.float32))
+            _ = env.formationsim_list[F - 1].agents
+        else:
+            env.reset_tensor()
+            env.rollout(torch.rand((4, A, 2), device=DEV) * 2 - 1)
+            env.metrics()
+        if i % 5 == 0:
+            env.release()
+        elif i % 5 == 1:
+            keep.append(env)  # left for the collector below
+        del env
+        if i % 10 == 9:
+            keep.clear()
+            gc.collect()
+    gc.collect()
+    torch.cuda.synchronize()
+    assert checked >= 8
+
+
+def test_env_dropped_inside_graph_capture(venv, flib):
+    """A handle dropped while a HIP graph is being captured is parked, not freed inside the
+    capture (which would invalidate it); the capture completes and replays, and the parked
+    handle is destroyed by the next create."""
+    keep = make_env(venv, 64, 5, reset_mode="philox")
+    keep.reset_tensor()
+    doomed = make_env(venv, 32, 5, reset_mode="philox")
+    doomed.reset_tensor()
+    acts = torch.rand((2, keep.num_envs, 2), device=DEV) * 2 - 1
+    obs = torch.empty((2, keep.num_envs, 8), device=DEV)
+    rew = torch.empty((2, keep.num_envs), device=DEV)
+    done = torch.empty((2, keep.num_envs), dtype=torch.bool, device=DEV)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        keep.rollout(acts, obs, rew, done)
+        del doomed  # its finalizer runs inside the capture
+    assert len(flib._deferred) == 1
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all()
+    make_env(venv, 2, 5).release()  # drains the parked handle
+    assert len(flib._deferred) == 0
+
+
+def test_view_touches_only_its_formation(venv):
+    """formationsim_list[i] on a 1,048,576 x 5 env reads formation i's slice only: the device
+    memory it allocates is O(N) (not the O(A) of get_state), and its values equal the full-state
+    rows and metrics."""
+    F, N = 1 << 20, 5
+    env = make_env(venv, F, N, reset_mode="philox", seed=3)
+    env.reset_tensor()
+    env.rollout(torch.rand((3, F * N, 2), device=DEV) * 2.4 - 1.2)
+    torch.cuda.synchronize()
+    i = 777_777
+    px, py, gx, gy, t = env.get_state()
+    full = env.metrics()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    v = env.formationsim_list[i]
+    ag, goal, sr = v.agents, v.goal, v.steps_since_reset
+    met, comp = v.compute_metrics(), v.reward_components()
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert peak < 64 * 1024, f"a view access allocated {peak} B of device memory"
+    sl = slice(i * N, (i + 1) * N)
+    assert torch.equal(ag, torch.stack([px[sl], py[sl]], 1).cpu())
+    assert torch.equal(goal, torch.stack([gx[i], gy[i]]).cpu())
+    assert sr == int(t[i])
+    row = full[i].tolist()
+    assert [met["avg_dist_to_goal"], met["ave_dist_to_neighbor"],
+            met["std_dist_to_neighbor"]] == row[:3]
+    assert list(comp.values()) == row[4:8]
+    # a range in the middle, with rewards, equals the same rows of the full call
+    rew = torch.rand(F * N, device=DEV)
+    a, b = 1000, 4096
+    assert torch.equal(env.metrics_range(a, b, rew[a * N:(a + b) * N]), env.metrics(rew)[a:a + b])
+    with pytest.raises(IndexError):
+        env.metrics_range(F - 1, 2)

@@ -1,0 +1,247 @@
+"""Round-3 PPO update tests on the GPU: per-instance exchange words (two updates on two streams of
+one device), the data-parallel gradient / apply kernels (ppo_grad, ppo_apply) against torch
+autograd and torch's Adam, the sharded update on the fused kernels against its eager form, and
+the fused update against torch at the reference's training configuration."""
+import ctypes
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def mods(pkg):
+    from importlib import import_module
+    return {m: import_module(pkg.__name__ + "." + m)
+            for m in ("vectorized_env", "policy", "ppo", "rollout", "dp_update", "_lib")}
+
+
+def _samples(n, D, seed):
+    g = torch.Generator().manual_seed(seed)
+    obs = (torch.rand((n, D), generator=g) * 2 - 1).to(DEV)
+    act = (torch.randn((n, 2), generator=g) * 0.7).to(DEV)
+    lp = (-torch.rand(n, generator=g) * 3 - 1).to(DEV)
+    adv = (torch.randn(n, generator=g) * 2).to(DEV)
+    ret = torch.randn(n, generator=g).to(DEV)
+    return obs, act, lp, adv, ret
+
+
+def _params(mods, D, seed=0):
+    pol = mods["policy"].MlpPolicy(D, device=DEV, seed=seed)
+    with torch.no_grad():
+        pol.flat.add_(torch.randn(pol.flat.shape, generator=torch.Generator().manual_seed(seed))
+                      .to(DEV) * 0.05)
+        pol.flat[-2:] = torch.tensor([-0.4, 0.2], device=DEV)
+    return pol.flat.clone()
+
+
+def _hp(L, cfg, lr=1e-3):
+    return L.PPOHParams(clip_range=cfg.clip_range, ent_coef=cfg.ent_coef, vf_coef=cfg.vf_coef,
+                        max_grad_norm=cfg.max_grad_norm, lr=lr, beta1=0.9, beta2=0.999, eps=1e-5,
+                        normalize_advantage=1)
+
+
+def test_two_updates_on_two_streams_equal_serial(mods):
+    """Two fused updates (different parameters, samples, permutations) running concurrently on
+    two streams of one device, each with its own workspace (ppo_update_ws), give the same bits as
+    the same two updates run one after the other; so does the legacy ppo_update, whose exchange
+    words are a stream-ordered allocation per launch (round 2 shared one set per device)."""
+    L = mods["_lib"]
+    lib = L.lib()
+    cfg = mods["ppo"].PPOConfig()
+    D, n, E = 8, 5000, 2
+    jobs = []
+    for k in range(2):
+        smp = _samples(n, D, 10 + k)
+        perm = torch.stack([torch.randperm(n, generator=torch.Generator().manual_seed(20 + 2 * k + e))
+                            for e in range(E)]).to(DEV)
+        jobs.append((_params(mods, D, k), smp, perm))
+
+    def run(concurrent, use_ws):
+        outs, streams, keep = [], [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)], []
+        torch.cuda.synchronize()
+        for k, (p0, smp, perm) in enumerate(jobs):
+            p = p0.clone()
+            m, v = torch.zeros_like(p), torch.zeros_like(p)
+            st = torch.zeros((), device=DEV)
+            sums = torch.zeros(4, dtype=torch.float64, device=DEV)
+            ws = torch.zeros(int(lib.ppo_workspace_bytes()), dtype=torch.uint8, device=DEV)
+            hp = _hp(L, cfg)
+            s = streams[k] if concurrent else torch.cuda.current_stream(DEV)
+            s.wait_stream(torch.cuda.current_stream(DEV))
+            args = [L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(st), D] + [L.ptr(t) for t in smp] + \
+                   [n, L.ptr(perm), E, 64, ctypes.byref(hp), L.ptr(sums)]
+            sp = ctypes.c_void_p(s.cuda_stream)
+            if use_ws:
+                L.check(lib.ppo_update_ws(*args, L.ptr(ws), sp), "ppo_update_ws")
+            else:
+                L.check(lib.ppo_update(*args, sp), "ppo_update")
+            keep.append(hp)
+            outs.append((p, m, v, st, sums))
+        torch.cuda.synchronize()
+        return outs
+
+    serial = run(False, True)
+    for use_ws in (True, False):
+        conc = run(True, use_ws)
+        for a, b in zip(serial, conc):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), use_ws
+    for _, _, _, _, sums in serial:
+        s = sums.tolist()
+        assert not math.isnan(s[0]) and s[3] >= 0  # no lost exchange
+
+
+@pytest.mark.parametrize("D", [8, 6])
+def test_ppo_grad_matches_autograd(mods, D):
+    """ppo_grad (the fused kernel in gradient mode) == torch autograd of the same rank-local loss
+    share (dp_update.ShardedUpdate._local_grad_eager): b_local = 24 of b_global = 64 samples,
+    global advantage statistics, the entropy term on (rank 0) and off; fp32 summation order and
+    the kernel's exp/rcp tanh (< 3e-7 absolute) are the only differences."""
+    L = mods["_lib"]
+    cfg = mods["ppo"].PPOConfig(batch_size=64, update_mode="sharded")
+    smp = _samples(300, D, 3)
+    flat = _params(mods, D, 1)
+    rows = torch.randperm(300, generator=torch.Generator().manual_seed(4))[:24].to(DEV)
+    for ent_once in (1, 0):
+        upd = mods["dp_update"].ShardedUpdate(cfg, D, [300], 0, DEV)
+        upd.rank = 0 if ent_once else 1
+        param = torch.nn.Parameter(flat.clone())
+        upd._local_grad_eager(param, smp, rows, 64, 0.3, 1.7)
+        want, want_sums = param.grad.clone(), upd.sums.clone()
+        grad = torch.full_like(flat, 7.0)
+        sums = torch.zeros(4, dtype=torch.float64, device=DEV)
+        hp = _hp(L, cfg)
+        L.check(L.lib().ppo_grad(L.ptr(flat), D, *(L.ptr(t) for t in smp), L.ptr(rows), 24, 64,
+                                 0.3, 1.7, 1, ent_once, ctypes.byref(hp), L.ptr(grad),
+                                 L.ptr(sums), L.current_stream(DEV)), "ppo_grad")
+        torch.cuda.synchronize()
+        scale = want.abs().max().item()
+        err = (grad - want).abs().max().item()
+        assert err <= 2e-6 * scale, (ent_once, err, scale)
+        torch.testing.assert_close(sums, want_sums, rtol=1e-5, atol=1e-7)
+    # no rows on this rank: a zero gradient (+ the entropy term where it lives)
+    grad = torch.full_like(flat, 7.0)
+    L.check(L.lib().ppo_grad(L.ptr(flat), D, *(L.ptr(t) for t in smp), None, 0, 64, 0.0, 1.0, 1,
+                             1, ctypes.byref(_hp(L, cfg)), L.ptr(grad), L.ptr(sums),
+                             L.current_stream(DEV)), "ppo_grad")
+    torch.cuda.synchronize()
+    assert torch.equal(grad[:-2], torch.zeros_like(grad[:-2]))
+    assert torch.equal(grad[-2:], torch.full((2,), -cfg.ent_coef, device=DEV))
+
+
+def test_ppo_apply_matches_torch_adam(mods):
+    """ppo_apply == torch clip_grad_norm_ + Adam(capturable) over 20 steps from the same
+    gradients (one clipped, one not, per step)."""
+    L = mods["_lib"]
+    cfg = mods["ppo"].PPOConfig()
+    flat = _params(mods, 8, 2)
+    param = torch.nn.Parameter(flat.clone())
+    opt = torch.optim.Adam([param], lr=1e-3, eps=1e-5, capturable=True)
+    p, m, v = flat.clone(), torch.zeros_like(flat), torch.zeros_like(flat)
+    st = torch.zeros((), device=DEV)
+    g = torch.Generator().manual_seed(9)
+    hp = _hp(L, cfg)
+    for k in range(20):
+        grad = (torch.randn(flat.shape, generator=g) * (0.001 if k % 2 else 0.05)).to(DEV)
+        param.grad = grad.clone()
+        torch.nn.utils.clip_grad_norm_([param], cfg.max_grad_norm)
+        opt.step()
+        L.check(L.lib().ppo_apply(L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(st), L.ptr(grad), 8,
+                                  ctypes.byref(hp), L.current_stream(DEV)), "ppo_apply")
+    torch.cuda.synchronize()
+    s = opt.state[param]
+    assert float(st) == float(s["step"]) == 20.0
+    torch.testing.assert_close(m, s["exp_avg"], rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(v, s["exp_avg_sq"], rtol=1e-5, atol=1e-12)
+    moved = (param.detach() - flat).abs().max().item()
+    assert moved > 1e-3
+    assert (p - param.detach()).abs().max().item() <= 1e-5 * moved
+
+
+def test_sharded_update_fused_equals_eager(mods):
+    """The data-parallel update on one rank (dp_update.ShardedUpdate.run): fused kernels
+    (ppo_grad + ppo_apply per minibatch) == torch autograd + torch Adam, 3 epochs over 1,000
+    samples in minibatches of 64 (the last one 40)."""
+    cfg = mods["ppo"].PPOConfig(n_epochs=3, update_mode="sharded")
+    smp = _samples(1000, 8, 5)
+    flat = _params(mods, 8, 3)
+    outs = []
+    for fused in (False, True):
+        param = torch.nn.Parameter(flat.clone())
+        opt = torch.optim.Adam([param], lr=1e-3, eps=1e-5, capturable=True)
+        upd = mods["dp_update"].ShardedUpdate(cfg, 8, [1000], 7, DEV, fused=fused)
+        stats = upd.run(param, opt, smp)
+        outs.append((param.detach().clone(), stats))
+    (p0, s0), (p1, s1) = outs
+    moved = (p0 - flat).abs().max().item()
+    err = (p1 - p0).abs().max().item()
+    assert moved > 1e-2 and err <= 1e-4 * moved, (moved, err)
+    for k in s0:
+        assert abs(s0[k] - s1[k]) <= 1e-4 * max(1.0, abs(s0[k])), (k, s0[k], s1[k])
+
+
+def test_fused_update_vs_torch_at_reference_config(mods):
+    """One full PPO update at the reference's training configuration
+    (/root/reference/vectorized_env.py:126-131: 1,000 formations x 5 agents, n_steps 10,
+    batch 64, 10 epochs = 7,820 dependent minibatches): the fused kernel (ppo_update) against
+    torch autograd + torch Adam (the HIP-graph replay of the eager minibatch step, equal to the
+    eager loop by test_graph_update_matches_eager) on the same samples and permutations.
+
+    The bound, per parameter: |p_fused - p_torch| <= 1e-3 * |p_torch - p_start| + 2e-5.
+    Derivation: one minibatch's gradients agree to ~1e-6 relative (fp32 summation order, the
+    kernel's exp/rcp tanh within 3e-7, tools/ppo_grad_debug.py); Adam divides by sqrt(v), so a
+    step differs by about lr x 1e-6 = 1e-9 and 7,820 steps accumulate at most ~1e-5 absolute
+    when nothing amplifies the difference (atol 2e-5).  Where training moves a parameter far,
+    the trajectories may separate slowly through the clipped ratio; relative to the distance
+    moved they must stay within 1e-3."""
+    cfg = {"num_formation": 1000, "num_agents_per_formation": 5, "goal_in_obs": True}
+    runs = []
+    for fused in (False, True):
+        env = mods["vectorized_env"].FormationEnv(cfg, device=DEV, seed=2, reset_mode="philox")
+        ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(), seed=3, use_graph=not fused,
+                              use_fused=fused)
+        flat0 = ppo.policy.flat.clone()
+        with torch.no_grad():
+            ppo.collector.collect()
+        st = ppo.train()
+        s = ppo.opt.state[ppo.param]
+        runs.append((flat0, ppo.policy.flat.clone(), st, float(s["step"])))
+        env.release()
+    (a0, p0, s0, k0), (a1, p1, s1, k1) = runs
+    assert torch.equal(a0, a1) and k0 == k1 == 7820
+    moved = (p0 - a0).abs()
+    err = (p1 - p0).abs()
+    excess = (err - (1e-3 * moved + 2e-5)).max().item()
+    print(f"\nreference-config update: max moved {moved.max().item():.4g}, max |diff| "
+          f"{err.max().item():.3g}, max |diff| / moved {(err / moved.clamp(min=1e-12)).max().item():.3g}, "
+          f"median |diff| {err.median().item():.3g}, losses torch {s0} fused {s1}")
+    assert excess <= 0, excess
+    for k in s0:
+        assert abs(s0[k] - s1[k]) <= 1e-4 * max(1.0, abs(s0[k])), (k, s0[k], s1[k])
+
+
+def test_ppo_sharded_mode_trains(mods):
+    """PPO(update_mode="sharded") on one rank: collect + train through the fused ppo_grad /
+    ppo_apply kernels; finite losses, the Adam step count of 2 updates x 3 epochs x 4 minibatches."""
+    env = mods["vectorized_env"].FormationEnv(
+        {"num_formation": 40, "num_agents_per_formation": 5, "goal_in_obs": True}, device=DEV,
+        seed=1, reset_mode="philox")
+    ppo = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(n_epochs=3, batch_size=512,
+                                                     update_mode="sharded"), seed=2)
+    assert ppo._dp is not None and ppo._dp.fused is False  # batch 512 > 64: the torch path
+    ppo2 = mods["ppo"].PPO(env, mods["ppo"].PPOConfig(n_epochs=3, batch_size=64,
+                                                      update_mode="sharded"), seed=2)
+    assert ppo2._dp.fused
+    for p in (ppo, ppo2):
+        for _ in range(2):
+            with torch.no_grad():
+                p.collector.collect()
+            st = p.train()
+            assert all(math.isfinite(v) for v in st.values()), st
+    assert float(ppo.opt.state[ppo.param]["step"]) == 2 * 3 * 4
+    assert float(ppo2.opt.state[ppo2.param]["step"]) == 2 * 3 * 32
+    env.release()
