@@ -54,7 +54,7 @@ inline void draw_formation(std::mt19937 &mt, int32_t N, float *px, float *py, fl
 
 // Device frees the runtime refused because a stream capture was under way (a hipFree inside a
 // capture is not allowed and would invalidate it): parked here, retried at the next
-// fenv_create / fenv_destroy, so fenv_destroy is safe to call at any point (DESIGN.md §10).
+// fenv_create / fenv_destroy, so fenv_destroy is safe to call at any point (DESIGN.md §9).
 struct Graveyard {
     std::mutex mu;
     std::vector<std::pair<int32_t, void *>> dev;   // (device, pointer) for hipFree

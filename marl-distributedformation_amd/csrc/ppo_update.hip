@@ -293,12 +293,19 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     const int64_t kMB = (n + bs - 1) / bs;
     const int64_t nmb = kMB * (int64_t)g.n_epochs;
     constexpr int OPT = (kPB * 8 + NT - 1) / NT;
-    auto perm_rows = [&](int64_t k, int64_t (&ro)[OPT], int64_t &rs) {  // rows this thread gathers
+    // minibatch positions (epoch, start) advance incrementally (no 64-bit division per minibatch)
+    auto advance = [&](int64_t &e, int64_t &sk) {
+        sk += bs;
+        if (sk >= n) {
+            sk = 0;
+            ++e;
+        }
+    };
+    auto perm_rows = [&](int64_t e, int64_t s0k, int64_t (&ro)[OPT], int64_t &rs) {  // rows this thread gathers
         rs = -1;
 #pragma unroll
         for (int j = 0; j < OPT; ++j) ro[j] = -1;
-        if (k >= nmb) return;
-        const int64_t e = k / kMB, s0k = (k - e * kMB) * bs;
+        if (e >= g.n_epochs) return;
         const int Bk = (int)((n - s0k) < bs ? (n - s0k) : bs);
         const int64_t *pp = g.perm + e * n + s0k;
 #pragma unroll
@@ -322,9 +329,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     int64_t ro_n[OPT], rs_n;  // perm rows of the next minibatch
     {
         int64_t ro0[OPT], rs0;
-        perm_rows(0, ro0, rs0);
+        perm_rows(0, 0, ro0, rs0);
         load_rows(ro0, rs0, po, ps);
-        perm_rows(1, ro_n, rs_n);
+        int64_t e1 = 0, s1 = 0;
+        advance(e1, s1);
+        perm_rows(e1, s1, ro_n, rs_n);
     }
     // Advantage normalisation of a Bk-sample minibatch (whole wave; lane l < Bk holds sample
     // l's advantage a).  It depends on the data only, so the split launch's actor block does it
@@ -340,6 +349,30 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         const float sd = __builtin_sqrtf(wsum(d * d) / (float)(Bk - 1));
         return (x - mean) / (sd + 1e-8f);
     };
+    int64_t e2 = 0, s2 = 0;  // position of minibatch kmb + 2
+    advance(e2, s2);
+    advance(e2, s2);
+    // Late gather (FENV_PPO_LATE_GATHER, split launch): the next minibatch's observations and
+    // per-sample inputs go to LDS at the END of a minibatch, after its last O / S read and
+    // while thread 0 waits on the norm exchange, instead of at the start of the next one.
+#ifndef FENV_PPO_LATE_GATHER
+#define FENV_PPO_LATE_GATHER 1
+#endif
+    constexpr bool kLate = SPLIT && !GRAD && FENV_PPO_LATE_GATHER;
+    auto gather_store = [&](int Bk, float adv_val) {
+#pragma unroll
+        for (int j = 0; j < OPT; ++j) {
+            const int e = tid + j * NT;
+            if (e < Bk * 8) O[(e >> 3) * 9 + (e & 7)] = po[j];
+        }
+        if (tid < Bk) {
+            S[sA0 * kPB + tid] = ps[0];
+            S[sA1 * kPB + tid] = ps[1];
+            S[sOLP * kPB + tid] = ps[2];
+            S[sADV * kPB + tid] = adv_val;
+            S[sRET * kPB + tid] = ps[4];
+        }
+    };
     float adv_nx = 0.0f;
     if (SPLIT && net_b == 0 && wl == 0) adv_nx = adv_norm((int)(n < bs ? n : bs), ps[3]);
     int64_t kmb = 0;
@@ -350,21 +383,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             const float invB = GRAD ? g.inv_bg : 1.0f / (float)B;
             float gss = 0.f;  // sum of squares of the gradient entries this thread writes
             // ---- gather the minibatch (from the prefetch registers), then start the next one
-#pragma unroll
-            for (int j = 0; j < OPT; ++j) {
-                const int e = tid + j * NT;
-                if (e < B * 8) O[(e >> 3) * 9 + (e & 7)] = po[j];
-            }
-            if (tid < B) {
-                S[sA0 * kPB + tid] = ps[0];
-                S[sA1 * kPB + tid] = ps[1];
-                S[sOLP * kPB + tid] = ps[2];
-                S[sADV * kPB + tid] = (SPLIT && net_b == 0) ? adv_nx : ps[3];
-                S[sRET * kPB + tid] = ps[4];
-            }
+            // (late gather: this minibatch's rows were stored at the end of the previous one)
+            if (!kLate || kmb == 0) gather_store(B, (SPLIT && net_b == 0) ? adv_nx : ps[3]);
             load_rows(ro_n, rs_n, po, ps);
-            perm_rows(kmb + 2, ro_n, rs_n);
-            __syncthreads();
+            perm_rows(e2, s2, ro_n, rs_n);
+            advance(e2, s2);
+            if (!kLate || kmb == 0) __syncthreads();
             FENV_PPO_PHASE(0);
             // ---- advantage normalisation (wave 0) || layer 1 (all waves)
             if (!SPLIT && w == 0 && hp.normalize_advantage && B > 1) {
@@ -814,6 +838,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 if (net_b == 0 && wl == 0 && kmb + 1 < nmb) {
                     const int64_t s1 = s0 + bs < n ? s0 + bs : 0;  // next minibatch's start
                     adv_nx = adv_norm((int)((n - s1) < bs ? (n - s1) : bs), ps[3]);
+                }
+                if constexpr (kLate) {  // the next minibatch's rows, under the exchange wait
+                    if (kmb + 1 < nmb) {
+                        const int64_t s1 = s0 + bs < n ? s0 + bs : 0;
+                        gather_store((int)((n - s1) < bs ? (n - s1) : bs),
+                                     net_b == 0 ? adv_nx : ps[3]);
+                    }
                 }
                 if (tid == 0) {
                     // after one timed-out wait the partner is taken as lost for good: no further

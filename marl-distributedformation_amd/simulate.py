@@ -11,7 +11,7 @@ size.  The simulation itself never runs through them.
 
 Views hold the env through a weak reference: an env and its views form no reference cycle, so a
 dropped env is freed by reference counting at a known point rather than by the cyclic garbage
-collector at an arbitrary one (DESIGN.md §10).
+collector at an arbitrary one (DESIGN.md §9).
 """
 from __future__ import annotations
 

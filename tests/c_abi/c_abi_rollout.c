@@ -135,6 +135,10 @@ static int run(int32_t N, int goal) {
 
 int main(void) {
     int ok = 1;
+    if (fenv_abi_version() != FENV_ABI_VERSION) {  /* built against another header revision */
+        fprintf(stderr, "libfenv ABI %d, header %d\n", fenv_abi_version(), FENV_ABI_VERSION);
+        return 1;
+    }
     /* error contract: a negative code and a message, nothing allocated */
     fenv_t *bad = (fenv_t *)0x1;
     const int rc = fenv_create(&bad, 0, 10, 0, 1, 0.25, 1000, 0, FENV_RESET_MT19937, 0, 0);

@@ -1,7 +1,7 @@
 """Env lifecycle on the GPU: deterministic release, teardown from
 the garbage collector and inside a HIP graph capture, and O(N) formation views.
 
-Round 2 saw one SIGABRT during garbage collection (DESIGN.md §10).  Envs then formed a reference
+Round 2 saw one SIGABRT during garbage collection (DESIGN.md §9).  Envs then formed a reference
 cycle with their formation views, so every dropped env -- its device state, its pinned host
 mirrors, its torch buffers -- was torn down by the cyclic collector at arbitrary points.  These
 tests churn a few hundred envs over every kernel path with explicit collections in between."""

@@ -26,8 +26,9 @@ import pkgload  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("case", choices=["t10", "t4same", "t4of10", "t10alt"])
 ap.add_argument("--launches", type=int, default=24)
-ap.add_argument("--alloc", choices=["torch", "onechunk"], default="torch",
-                help="onechunk: every plane of a set carved from one allocation")
+ap.add_argument("--alloc", choices=["torch", "onechunk", "contig"], default="torch",
+                help="onechunk: every plane of a set carved from one torch allocation; contig: "
+                     "each buffer from hipExtMallocWithFlags(hipDeviceMallocContiguous)")
 args = ap.parse_args()
 
 pkg = pkgload.load()
@@ -42,7 +43,43 @@ env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N, "goa
 env.reset_tensor()
 
 
+class _Raw:
+    """A hipExtMallocWithFlags buffer exposed to torch through __cuda_array_interface__."""
+    hip = None
+
+    def __init__(self, shape, dtype, flags):
+        import ctypes
+        if _Raw.hip is None:
+            _Raw.hip = ctypes.CDLL("libamdhip64.so")
+        n = 1
+        for d in shape:
+            n *= d
+        esz = torch.empty((), dtype=dtype).element_size()
+        self.p = ctypes.c_void_p()
+        rc = _Raw.hip.hipExtMallocWithFlags(ctypes.byref(self.p), ctypes.c_size_t(n * esz),
+                                           ctypes.c_uint(flags))
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags rc={rc}")
+        typestr = {torch.float32: "<f4", torch.bool: "|b1"}[dtype]
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr,
+                                         "data": (self.p.value, False), "version": 2}
+
+
+_keep = []
+
+
+def raw_tensor(shape, dtype):
+    r = _Raw(shape, dtype, 0x4)  # hipDeviceMallocContiguous
+    _keep.append(r)
+    return torch.as_tensor(r, device=dev)
+
+
 def bufset(P):
+    if args.alloc == "contig":
+        act = raw_tensor((P, A, 2), torch.float32)
+        act.uniform_(-1, 1)
+        return (act, raw_tensor((P, A, D), torch.float32), raw_tensor((P, A), torch.float32),
+                raw_tensor((P, A), torch.bool))
     if args.alloc == "onechunk":
         per = A * (2 * 4 + D * 4 + 4 + 1) + 4 * 4096
         raw = torch.empty(P * per, dtype=torch.uint8, device=dev)
