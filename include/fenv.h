@@ -34,7 +34,7 @@ extern "C" {
  * gets a new symbol name, never a reordered argument list under the old one.
  *   1  round-1/2 entry points (policy_forward with row0)
  *   2  + fenv_abi_version, fenv_get_state_range, fenv_metrics_range, ppo_workspace_bytes,
- *        ppo_update_ws, ppo_grad, ppo_apply */
+ *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject */
 #define FENV_ABI_VERSION 2
 int fenv_abi_version(void);
 
@@ -287,6 +287,11 @@ int ppo_grad(const float *params, int32_t obs_dim, const float *obs, const float
              float *grad, double *stats, void *stream);
 int ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, float *step, const float *grad,
               int32_t obs_dim, const ppo_hparams *hp, void *stream);
+
+/* Test hook: the next n_launches fused PPO updates (ppo_update / ppo_update_ws) run as if the two
+ * workgroups' norm exchange were lost (the critic never posts; the actor's wait is short), so
+ * the NaN-poisoned-update / restore / re-run / raise paths of a caller can be exercised. */
+void fenv_test_ppo_inject(int32_t n_launches);
 
 const char *fenv_last_error(void);
 

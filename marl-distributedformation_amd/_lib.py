@@ -66,6 +66,7 @@ SIGNATURES = {
     "ppo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.c_float,
                         ctypes.c_float, _I32, _I32, _P, _P, _P, _P]),
     "ppo_apply": (_I32, [_P, _P, _P, _P, _P, _I32, _P, _P]),
+    "fenv_test_ppo_inject": (None, [_I32]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
 

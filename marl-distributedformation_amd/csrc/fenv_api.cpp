@@ -643,6 +643,8 @@ int ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step, in
 
 int64_t ppo_workspace_bytes(void) { return (int64_t)fenvk::ppo_workspace_bytes_impl(); }
 
+void fenv_test_ppo_inject(int32_t n_launches) { fenvk::ppo_set_inject(n_launches); }
+
 int ppo_update_ws(float *params, float *exp_avg, float *exp_avg_sq, float *step, int32_t obs_dim,
                   const float *obs, const float *actions, const float *old_log_prob,
                   const float *advantages, const float *returns, int64_t n, const int64_t *perm,

@@ -124,6 +124,7 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
                              int32_t batch_size, const ppo_hparams &hp, double *stats,
                              void *workspace, hipStream_t st);
 size_t ppo_workspace_bytes_impl();
+void ppo_set_inject(int n);
 hipError_t launch_ppo_grad(const float *params, int32_t D, const float *obs, const float *act,
                            const float *old_log_prob, const float *adv, const float *ret,
                            const int64_t *rows, int32_t b_local, int32_t b_global,

@@ -39,6 +39,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -97,6 +98,9 @@ struct PPOArgs {
     float *grad;
     float inv_bg, adv_mean, adv_std;
     int32_t adv_norm_on, ent_once;
+    // test hook (fenv_test_ppo_inject): the critic block never posts its partial and the actor's
+    // wait budget is short, so the launch ends as a lost exchange does
+    int32_t inject_lost;
 };
 
 // Split launch (FENV_PPO_SPLIT): the actor and the critic each on their own CU.  The two networks'
@@ -273,6 +277,29 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             const int p = own(q);
             lp[q] = p < P ? lx(p) : kPadIx;
         }
+    }
+    // log_std-derived constants of the loss (FENV_PPO_LOSS_PRE): exp, its square, its log and
+    // the reciprocals, per action component, kept in LDS R[kLS + 5 j + ...] by the thread that
+    // updates log_std_j (at the end of its Adam step), so the loss wave's dependent chain starts
+    // from them instead of computing two expf and two logf per minibatch
+#ifndef FENV_PPO_LOSS_PRE
+#define FENV_PPO_LOSS_PRE 0
+#endif
+    constexpr int kLS = 40;
+    auto ls_consts = [&](int j, float ls) {
+        const float sd = expf(ls);
+        const float var = sd * sd;
+        R[kLS + 5 * j + 0] = var;
+        R[kLS + 5 * j + 1] = logf(sd);  // torch: std.log()
+        R[kLS + 5 * j + 2] = 1.0f / (2.0f * var);
+        R[kLS + 5 * j + 3] = 1.0f / var;
+    };
+    if (FENV_PPO_LOSS_PRE && tid < 2) ls_consts(tid, g.params[L.logstd + tid]);
+    int ls_j = -1;  // the log_std component whose Adam slot this thread owns, if any
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        const int pq = own(q);
+        if (pq >= L.logstd && pq < L.logstd + 2) ls_j = pq - L.logstd;
     }
     bool partner_lost = false;  // split launch: the other block's norm exchange timed out
     const float lb1 = log2f(hp.beta1), lb2 = log2f(hp.beta2);
@@ -503,10 +530,19 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if (wl == 0) {
                 const bool do_pi = !SPLIT || net_b == 0, do_vf = !SPLIT || net_b == 1;
                 const bool on = lane < B;
+#if FENV_PPO_LOSS_PRE
+                const float var0 = R[kLS + 0], lsd0 = R[kLS + 1], i2v0 = R[kLS + 2], iv0 = R[kLS + 3];
+                const float var1 = R[kLS + 5], lsd1 = R[kLS + 6], i2v1 = R[kLS + 7], iv1 = R[kLS + 8];
+                (void)var0;
+                (void)var1;
+#else
                 const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
                 const float sd0 = expf(ls0), sd1 = expf(ls1);
                 const float var0 = sd0 * sd0, var1 = sd1 * sd1;
                 const float lsd0 = logf(sd0), lsd1 = logf(sd1);  // torch: std.log()
+                const float i2v0 = 1.0f / (2.0f * var0), i2v1 = 1.0f / (2.0f * var1);
+                const float iv0 = 1.0f / var0, iv1 = 1.0f / var1;
+#endif
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
                 if (on) {
@@ -515,8 +551,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
                     const float d0 = a0 - mu0, d1 = a1 - mu1;
                     const float kLogSqrt2Pi = 0.918938533204672742f;
-                    const float lp = (-(d0 * d0) / (2.0f * var0) - lsd0 - kLogSqrt2Pi) +
-                                     (-(d1 * d1) / (2.0f * var1) - lsd1 - kLogSqrt2Pi);
+                    // divisions by 2 var and var as products with their reciprocals (1 ulp)
+                    const float lp = (-(d0 * d0) * i2v0 - lsd0 - kLogSqrt2Pi) +
+                                     (-(d1 * d1) * i2v1 - lsd1 - kLogSqrt2Pi);
                     const float ratio = expf(lp - S[sOLP * kPB + lane]);
                     const float an = S[sADV * kPB + lane];
                     const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
@@ -533,10 +570,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     const float dratio = -(g1 * an + g2 * an * inside) * invB;
                     const float dlp = dratio * ratio;
                     gv = hp.vf_coef * (-2.0f * rr) * invB;
-                    gmu0 = dlp * d0 / var0;
-                    gmu1 = dlp * d1 / var1;
-                    gls0 = dlp * (d0 * d0 / var0 - 1.0f);
-                    gls1 = dlp * (d1 * d1 / var1 - 1.0f);
+                    gmu0 = dlp * (d0 * iv0);
+                    gmu1 = dlp * (d1 * iv1);
+                    gls0 = dlp * ((d0 * d0) * iv0 - 1.0f);
+                    gls1 = dlp * ((d1 * d1) * iv1 - 1.0f);
                 }
                 if (do_pi) {
                     S[sGMU0 * kPB + lane] = gmu0;
@@ -826,6 +863,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     // two words per block, by minibatch parity: the partner's word for this
                     // minibatch cannot be overwritten before this block has read it (its next
                     // post to the same word is two minibatches on, which waits on this block)
+                    if (!(g.inject_lost && net_b == 1))
                     __hip_atomic_store(g.xch + 2 * net_b + (kmb & 1),
                                        (seq << 32) | __float_as_uint(tot), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
@@ -850,7 +888,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     // after one timed-out wait the partner is taken as lost for good: no further
                     // waits, so a broken launch ends in milliseconds, not one timeout per
                     // minibatch
-                    const int max_spin = partner_lost ? 0 : (1 << 22);
+                    const int max_spin = partner_lost ? 0 : (g.inject_lost ? (1 << 10) : (1 << 22));
                     for (int spin = 0; spin < max_spin && (o >> 32) != seq; ++spin) {
                         __builtin_amdgcn_s_sleep(1);
                         o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
@@ -884,9 +922,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
                     // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
                     const float den = __builtin_amdgcn_sqrtf(v[q]) * inv_bc2s + hp.eps;
-                    W[ix] = (SPLIT ? wq[q] : W[ix]) - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
+                    const float wn = (SPLIT ? wq[q] : W[ix]) - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
+                    W[ix] = wn;
                 }
             }
+            // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
+            if (FENV_PPO_LOSS_PRE && !GRAD && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
             __syncthreads();
             FENV_PPO_PHASE(10);
         }
@@ -996,6 +1037,16 @@ static bool split_fits(int32_t D) {
 
 size_t ppo_workspace_bytes_impl() { return 4 * sizeof(uint64_t); }
 
+// test hook: the next n fused-update launches (any device / thread) lose their norm exchange
+static std::atomic<int> g_inject_lost{0};
+void ppo_set_inject(int n) { g_inject_lost.store(n < 0 ? 0 : n); }
+static int ppo_take_inject() {
+    int v = g_inject_lost.load();
+    while (v > 0 && !g_inject_lost.compare_exchange_weak(v, v - 1)) {
+    }
+    return v > 0 ? 1 : 0;
+}
+
 hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, float *step,
                              int32_t D, const float *obs, const float *act,
                              const float *old_log_prob, const float *adv, const float *ret,
@@ -1022,7 +1073,8 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
         if (e != hipSuccess) return e;
     }
     PPOArgs g{params, exp_avg, exp_avg_sq, step, obs, act, old_log_prob, adv, ret, perm, n,
-              D, n_epochs, batch_size, hp, stats, xch, nullptr, 0.f, 0.f, 1.f, 0, 1};
+              D, n_epochs, batch_size, hp, stats, xch, nullptr, 0.f, 0.f, 1.f, 0, 1,
+              split ? ppo_take_inject() : 0};
     if (split)
         hipLaunchKernelGGL(k_ppo_update<true>, dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
     else
@@ -1047,7 +1099,7 @@ hipError_t launch_ppo_grad(const float *params, int32_t D, const float *obs, con
     PPOArgs g{const_cast<float *>(params), nullptr, nullptr, nullptr, obs, act, old_log_prob,
               adv, ret, rows, (int64_t)b_local, D, 1, b_local, hp, stats, nullptr, grad,
               1.0f / (float)b_global, adv_mean, adv_std,
-              (adv_normalize && b_global > 1) ? 1 : 0, entropy_term ? 1 : 0};
+              (adv_normalize && b_global > 1) ? 1 : 0, entropy_term ? 1 : 0, 0};
     hipLaunchKernelGGL((k_ppo_update<true, true>), dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
     return hipGetLastError();
 }

@@ -305,9 +305,14 @@ class PPO:
             with torch.no_grad():
                 for t, s in zip(state, snap):
                     t.copy_(s)
+        bad = math.isnan(m[0])
         if self.world > 1:  # any rank's NaN makes every rank raise
-            bad = pdist.max_over_ranks(1.0 if math.isnan(m[0]) else 0.0, dev) > 0
-            if bad and not math.isnan(m[0]):
+            bad = pdist.max_over_ranks(1.0 if bad else 0.0, dev) > 0
+        if bad:  # leave the pre-update parameters and Adam state, not NaN-poisoned ones
+            with torch.no_grad():
+                for t, s in zip(state, snap):
+                    t.copy_(s)
+            if not math.isnan(m[0]):
                 raise RuntimeError("fused PPO update failed on another rank")
         if math.isnan(m[0]):
             raise RuntimeError("fused PPO update: NaN policy loss (" +

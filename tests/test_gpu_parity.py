@@ -283,10 +283,20 @@ def test_metrics_and_partials(venv, F, N):
     partial = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
     obs, rew, done = env.rollout(torch.from_numpy(acts).to(DEV), partial=partial)
     rs, ds = 0.0, 0.0
+    r = rew.cpu().numpy()
     for k in range(8):
         _, rr, rd, _ = ref.step(acts[k])
         rs += rr.astype(np.float64).sum()
         ds += rd.sum()
+        # rewards first, bit for bit: a record mismatch below is then the records' own
+        assert np.array_equal(r[k].view(np.uint32), rr.view(np.uint32)), f"rewards, step {k}"
+    recs = partial.cpu().numpy().astype(np.float64)
+    if N <= 64:  # one record per 4 formation-waves: each equals its agents' reward sum
+        per = 4 * (64 // N) * N
+        own = np.array([r[:, g * per:(g + 1) * per].astype(np.float64).sum()
+                        for g in range(recs.shape[0])])
+        bad = np.nonzero(np.abs(recs[:, 0] - own) > 1e-5 * np.abs(own).max())[0]
+        assert bad.size == 0, f"records {bad.tolist()}: {recs[bad, 0]} vs {own[bad]}"
     sums = env.reduce_partials(partial).cpu().numpy()
     np.testing.assert_allclose(sums[0], rs, rtol=1e-5)
     assert sums[1] == ds
