@@ -402,6 +402,54 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     };
     float adv_nx = 0.0f;
     if (SPLIT && net_b == 0 && wl == 0) adv_nx = adv_norm((int)(n < bs ? n : bs), ps[3]);
+    // Adam split (FENV_PPO_ADAM_SPLIT, split launch): a minibatch's Adam step updates the slots
+    // holding layer 1 (W1, b1: slots 0..kKA-1 of every thread, PLayout puts them first) before
+    // the barrier, and the other slots (W2, b2, heads, log_std) only in the next minibatch's
+    // layer-1 phase, whose MFMAs and tanh never read them: the scheduler fills layer 1's
+    // latencies with the register-only Adam arithmetic.  Same operations, same results.
+#ifndef FENV_PPO_ADAM_SPLIT
+#define FENV_PPO_ADAM_SPLIT 1
+#endif
+    constexpr bool kAS = SPLIT && !GRAD && FENV_PPO_ADAM_SPLIT;
+    constexpr int kKA = kAS ? 3 : KP;  // ceil((64 D + 64) / 256) <= 3 for D <= 8
+    // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
+#ifndef FENV_PPO_EARLY_X
+#define FENV_PPO_EARLY_X 0
+#endif
+#ifndef FENV_PPO_ADAM_FMA
+#define FENV_PPO_ADAM_FMA 0
+#endif
+    float a_coef = 0.f, a_ss = 0.f, a_ib = 0.f;  // clip coef, step size, 1/sqrt(bc2)
+    float gq[SPLIT ? KP : 1], wq[SPLIT ? KP : 1];
+    auto adam_slot = [&](int q) {
+        const int p = SPLIT ? 0 : own(q);  // split: every slot (spare ones hit the pad)
+        if (p < P) {
+            const int ix = SPLIT ? lp[q] : lx(p);
+            const float gr = (SPLIT ? gq[q] : G[ix]) * a_coef;
+#if FENV_PPO_ADAM_FMA
+            m[q] = __builtin_fmaf(1.0f - hp.beta1, gr - m[q], m[q]);
+            v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q] * hp.beta2);
+            const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v[q]), a_ib, hp.eps);
+            const float wn = __builtin_fmaf(-a_ss, m[q] * __builtin_amdgcn_rcpf(den),
+                                            SPLIT ? wq[q] : W[ix]);
+#else
+            m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
+            v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
+            // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
+            // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
+            const float den = __builtin_amdgcn_sqrtf(v[q]) * a_ib + hp.eps;
+            const float wn = (SPLIT ? wq[q] : W[ix]) - a_ss * (m[q] * __builtin_amdgcn_rcpf(den));
+#endif
+            W[ix] = wn;
+        }
+    };
+    // the deferred slots of the previous minibatch's Adam step (kAS)
+    auto adam_rest = [&]() {
+#pragma unroll
+        for (int q = kKA; q < KP; ++q) adam_slot(q);
+        // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
+        if (FENV_PPO_LOSS_PRE && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
+    };
     int64_t kmb = 0;
     for (int ep = 0; ep < g.n_epochs; ++ep) {
         for (int64_t s0 = 0; s0 < n; s0 += bs, ++kmb) {
@@ -409,6 +457,15 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // loss means: over this minibatch, or (gradient mode) over the global minibatch
             const float invB = GRAD ? g.inv_bg : 1.0f / (float)B;
             float gss = 0.f;  // sum of squares of the gradient entries this thread writes
+            // split: the partner's exchange word read ahead of this block's own post
+            // (FENV_PPO_EARLY_X 1: before the norm's wave sum, 2: before the W1 gradients); the
+            // actor usually arrives after the critic has posted, so its wait starts resolved
+            uint64_t o_early = 0;
+            auto early_load = [&]() {
+                if (SPLIT && !GRAD && tid == 0 && !partner_lost)
+                    o_early = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
             // ---- gather the minibatch (from the prefetch registers), then start the next one
             // (late gather: this minibatch's rows were stored at the end of the previous one)
             if (!kLate || kmb == 0) gather_store(B, (SPLIT && net_b == 0) ? adv_nx : ps[3]);
@@ -428,7 +485,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // layer 1 on v_mfma_f32_16x16x4f32: wave w = net w>>2, hidden units 16(w&3)..+15, all
             // 64 sample rows as 4 tiles; K = 8 obs columns (zero-padded past D) as 2 MFMAs.  The
             // W1 operand past column D reads the next row's weights, multiplied by O's zeros.
-            {
+            auto layer1 = [&]() {
                 const int net = w >> 2, jt = w & 3, q = lane >> 4, c = lane & 15;
                 const int j = 16 * jt + c;
                 const int w1 = (net ? L.vf0W : L.pi0W) + j * D + q;
@@ -444,6 +501,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) hr[r * kRow] = tanh_u(acc[r]);
                 }
+            };
+            // kAS: the previous minibatch's deferred Adam slots in the same straight-line block
+            // as layer 1 (one basic block, so the two interleave)
+            if (kAS && kmb > 0) {
+                layer1();
+                adam_rest();
+            } else {
+                layer1();
             }
             __syncthreads();
             FENV_PPO_PHASE(1);
@@ -779,6 +844,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(7);
+            if (FENV_PPO_EARLY_X == 2) early_load();
             // ---- W1 gradients GW1 = dZ1^T . O on v_mfma_f32_16x16x4f32 (wave w: net w>>2, hidden
             // rows 16(w&3)..+15, obs columns 0..15 of which 0..D-1 are real; K = 64 samples,
             // slot q <-> sample 16q + i) and b1 gradients
@@ -835,13 +901,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- clip_grad_norm_(max_grad_norm): global 2-norm from the squares each thread
             // accumulated as it wrote its gradient entries (every entry is written exactly once
             // per minibatch), one wave sum each, reduced after the barrier
+            if (FENV_PPO_EARLY_X == 1) early_load();
             gss = wsum(gss);
             if (lane == 0) R[wl] = gss;
             __syncthreads();
             FENV_PPO_PHASE(8);
             // split: this thread's gradient and parameter entries are read now, so the LDS
             // reads overlap the norm exchange below
-            float gq[SPLIT ? KP : 1], wq[SPLIT ? KP : 1];
             if constexpr (SPLIT) {
 #pragma unroll
                 for (int q = 0; q < KP; ++q) {
@@ -867,9 +933,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     __hip_atomic_store(g.xch + 2 * net_b + (kmb & 1),
                                        (seq << 32) | __float_as_uint(tot), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    if (!partner_lost)
-                        o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!partner_lost) {
+                        if (FENV_PPO_EARLY_X && (o_early >> 32) == seq)
+                            o = o_early;
+                        else
+                            o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
                 // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
                 // at this minibatch's gather) while the first load is in flight
@@ -909,28 +979,21 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             step += 1.0f;
             const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
             const float bc2 = 1.0f - exp2f(step * lb2);
-            const float step_size = hp.lr / bc1;
-            const float inv_bc2s = 1.0f / __builtin_sqrtf(bc2);
+            a_coef = coef;
+            a_ss = hp.lr / bc1;
+            a_ib = 1.0f / __builtin_sqrtf(bc2);
+            // kAS: slots 0..kKA-1 (layer 1) now, the rest in the next minibatch's layer-1 phase
 #pragma unroll
-            for (int q = 0; q < KP; ++q) {
-                const int p = SPLIT ? 0 : own(q);  // split: every slot (spare ones hit the pad)
-                if (p < P) {
-                    const int ix = SPLIT ? lp[q] : lx(p);
-                    const float gr = (SPLIT ? gq[q] : G[ix]) * coef;
-                    m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
-                    v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
-                    // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
-                    // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
-                    const float den = __builtin_amdgcn_sqrtf(v[q]) * inv_bc2s + hp.eps;
-                    const float wn = (SPLIT ? wq[q] : W[ix]) - step_size * (m[q] * __builtin_amdgcn_rcpf(den));
-                    W[ix] = wn;
-                }
-            }
+            for (int q = 0; q < kKA; ++q) adam_slot(q);
             // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
-            if (FENV_PPO_LOSS_PRE && !GRAD && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
+            if (!kAS && FENV_PPO_LOSS_PRE && !GRAD && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
             __syncthreads();
             FENV_PPO_PHASE(10);
         }
+    }
+    if constexpr (kAS) {  // the last minibatch's deferred Adam slots
+        if (kmb > 0) adam_rest();
+        __syncthreads();
     }
 #pragma unroll
     for (int q = 0; q < KP; ++q) {

@@ -74,7 +74,21 @@ def run(kind):
     bad_state = [i for i, (a, b) in enumerate(zip(st, rst)) if not np.array_equal(a, b)]
     nbad = int((st[0] != rst[0]).sum()) if 0 in bad_state else 0
     first_idx = int(np.nonzero(st[0] != rst[0])[0][0]) if nbad else -1
-    print(f"{kind:6s}: reset obs ok {obs_reset_ok}; first reward mismatch {first_bad}; state after the "
+    src = ""
+    if nbad:  # which MT reset set the launch applied to the wrong agents (2 is right)
+        import ctypes
+        L = lib.lib()
+        bad = np.nonzero(st[0] != rst[0])[0]
+        for s_ in (0, 1, 2, 3, 4):
+            hp = np.zeros(F * N, np.float32); hq = np.zeros(F * N, np.float32)
+            g1 = np.zeros(F, np.float32); g2 = np.zeros(F, np.float32)
+            f = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+            L.fenv_host_reset_draws(ctypes.c_uint32(21), ctypes.c_int64(s_), ctypes.c_int64(F),
+                                    ctypes.c_int64(0), ctypes.c_int64(F), ctypes.c_int32(N),
+                                    f(hp), f(hq), f(g1), f(g2))
+            src += f" set{s_}:{int((st[0][bad] == hp[bad]).sum())}/{bad.size}"
+        src += f" bad agents {bad[:8].tolist()}..{bad[-1]}"
+    print(f"{kind:6s}: reset obs ok {obs_reset_ok}; first reward mismatch {first_bad};{src} state after the "
           f"in-launch reset differs in fields {bad_state} (px: {nbad} agents, first {first_idx})",
           flush=True)
     env.release()
