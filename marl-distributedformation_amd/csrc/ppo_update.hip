@@ -412,6 +412,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
     constexpr bool kAS = SPLIT && !GRAD && FENV_PPO_ADAM_SPLIT;
     constexpr int kKA = kAS ? 3 : KP;  // ceil((64 D + 64) / 256) <= 3 for D <= 8
+    // dL/dz1 in the other network's H1 half (FENV_PPO_DZ1_SEP, split launch: each block owns
+    // the whole LDS image but runs one network, so that half is free)
+#ifndef FENV_PPO_DZ1_SEP
+#define FENV_PPO_DZ1_SEP 1
+#endif
+    constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
+    const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
 #ifndef FENV_PPO_EARLY_X
 #define FENV_PPO_EARLY_X 0
@@ -833,13 +840,16 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     G[lx((bn ? L.vf2b : L.pi2b) + j)] = acc;
                     gss = __builtin_fmaf(acc, acc, gss);
                 }
-                __syncthreads();
+                // kZ1S: dL/dz1 goes to the other network's (unused) H1 half, so no wave's write can
+                // overtake another wave's GW2 reads of h1 and no barrier is needed here
+                if (!kZ1S) __syncthreads();
                 FENV_PPO_PHASE(6);
-                float *H1r = H1 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
+                const float *H1r = H1 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
+                float *Z1w = H1 + ((kZ1S ? zb : net) * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float hv = H1r[rho(r, h) * kRow];
-                    H1r[rho(r, h) * kRow] = dz[r] * (1.0f - hv * hv);
+                    Z1w[rho(r, h) * kRow] = dz[r] * (1.0f - hv * hv);
                 }
             }
             __syncthreads();
@@ -850,7 +860,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // slot q <-> sample 16q + i) and b1 gradients
             {
                 const int net = w >> 2, jt = w & 3, q = lane >> 4, c = lane & 15;
-                const float *Z1 = H1 + net * kPB * kRow + 16 * jt + c;
+                const float *Z1 = H1 + (kZ1S ? zb : net) * kPB * kRow + 16 * jt + c;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                 if constexpr (SPLIT) {  // operands read up front, branch-free (see head grads)
                     float zv[16], ov[16];
@@ -884,7 +894,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             if (tid < (SPLIT ? kHid : 2 * kHid)) {
                 const int net = SPLIT ? net_b : tid >> 6, j = tid & 63;
-                const float *z1 = H1 + net * kPB * kRow + j;
+                const float *z1 = H1 + (kZ1S ? (net ^ 1) : net) * kPB * kRow + j;
                 const float acc = col_sum(z1, B);
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
                 gss = __builtin_fmaf(acc, acc, gss);
