@@ -418,6 +418,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_SEP 1
 #endif
     constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
+#ifndef FENV_PPO_LS_EARLY
+#define FENV_PPO_LS_EARLY 1
+#endif
+    constexpr bool kLE = FENV_PPO_LS_EARLY && !FENV_PPO_LOSS_PRE;
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
 #ifndef FENV_PPO_EARLY_X
@@ -563,6 +567,24 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
             // v_mfma_f32_16x16x4f32: wave w = net w>>2, samples 16(w&3)..+15, output columns 0..15
             // of which 2 (actor) / 1 (critic) are real; K = 64 hidden as 16 MFMAs
+            // The loss's log_std-derived constants (FENV_PPO_LS_EARLY) are computed here, under the
+            // head MFMAs, by every wave (wave 0 keeps them for the loss phase): log_std was final
+            // at the layer-1 barrier, and the loss wave's chain then starts from the samples.
+            float lc_var0 = 0.f, lc_var1 = 0.f, lc_lsd0 = 0.f, lc_lsd1 = 0.f;
+            float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
+            auto loss_consts = [&]() {
+                const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
+                const float sd0 = expf(ls0), sd1 = expf(ls1);
+                lc_var0 = sd0 * sd0;
+                lc_var1 = sd1 * sd1;
+                lc_lsd0 = logf(sd0);  // torch: std.log()
+                lc_lsd1 = logf(sd1);
+                lc_i2v0 = 1.0f / (2.0f * lc_var0);
+                lc_i2v1 = 1.0f / (2.0f * lc_var1);
+                lc_iv0 = 1.0f / lc_var0;
+                lc_iv1 = 1.0f / lc_var1;
+            };
+            if (kLE) loss_consts();
             {
                 const int net = w >> 2, bt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
@@ -608,12 +630,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 (void)var0;
                 (void)var1;
 #else
-                const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
-                const float sd0 = expf(ls0), sd1 = expf(ls1);
-                const float var0 = sd0 * sd0, var1 = sd1 * sd1;
-                const float lsd0 = logf(sd0), lsd1 = logf(sd1);  // torch: std.log()
-                const float i2v0 = 1.0f / (2.0f * var0), i2v1 = 1.0f / (2.0f * var1);
-                const float iv0 = 1.0f / var0, iv1 = 1.0f / var1;
+                if (!kLE) loss_consts();
+                const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
+                const float iv0 = lc_iv0, iv1 = lc_iv1;
+                (void)lc_var0;
+                (void)lc_var1;
 #endif
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
