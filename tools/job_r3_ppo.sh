@@ -13,4 +13,4 @@ for v in 1 2; do
   echo "== PPO phase profile, block $v"
   FENV_LIB_OVERRIDE=$PWD/build_variants/libfenv_nprof$v.so timeout -k 10 100 python -u tools/ppo_phase_profile.py || exit $?
 done
-PAIRS=${PAIRS:-3} VARIANTS="${PPO_VARIANTS:-old as0 zs0 le0 ex1 ex2 fma}" timeout -k 10 700 bash tools/ppo_variant_ab.sh | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//"
+PAIRS=${PAIRS:-2} VARIANTS="${PPO_VARIANTS:-old as0 zs0 le0 ex1 ex2 fma}" timeout -k 10 700 bash tools/ppo_variant_ab.sh | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//"
