@@ -418,6 +418,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_SEP 1
 #endif
     constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
+#ifndef FENV_PPO_HG_VEC
+#define FENV_PPO_HG_VEC 1
+#endif
 #ifndef FENV_PPO_LS_EARLY
 #define FENV_PPO_LS_EARLY 1
 #endif
@@ -722,14 +725,34 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *sg = S + (net ? sGV : sGMU0 + (c & 1)) * kPB;
                 const float *s0p = S + (net ? sGV : sGMU0) * kPB, *s1p = S + sGMU1 * kPB;
                 float ha[16], sb[16], s0[16], s1[16];
+                // sample of K-step t: b = 16 q + t (FENV_PPO_HG_VEC: the per-sample scalars of a
+                // lane group are then 16 contiguous floats, read as four ds_read_b128) or 4 t + q
+                auto bidx = [&](int t) { return FENV_PPO_HG_VEC ? 16 * q + t : 4 * t + q; };
+#pragma unroll
+                for (int t = 0; t < 16; ++t) ha[t] = hcol[bidx(t) * kRow + c];
+#if FENV_PPO_HG_VEC
+                {
+                    const float4 *g4 = reinterpret_cast<const float4 *>(sg + 16 * q);
+                    const float4 *a4 = reinterpret_cast<const float4 *>(s0p + 16 * q);
+                    const float4 *c4 = reinterpret_cast<const float4 *>(s1p + 16 * q);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float4 x = g4[j], y = a4[j];
+                        const float4 z = net ? make_float4(0.f, 0.f, 0.f, 0.f) : c4[j];
+                        sb[4 * j] = x.x; sb[4 * j + 1] = x.y; sb[4 * j + 2] = x.z; sb[4 * j + 3] = x.w;
+                        s0[4 * j] = y.x; s0[4 * j + 1] = y.y; s0[4 * j + 2] = y.z; s0[4 * j + 3] = y.w;
+                        s1[4 * j] = z.x; s1[4 * j + 1] = z.y; s1[4 * j + 2] = z.z; s1[4 * j + 3] = z.w;
+                    }
+                }
+#else
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const int b = 4 * t + q;
-                    ha[t] = hcol[b * kRow + c];
+                    const int b = bidx(t);
                     sb[t] = sg[b];
                     s0[t] = s0p[b];
                     s1[t] = net ? 0.0f : s1p[b];
                 }
+#endif
                 const int k = 16 * kt + c;
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
                 const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
@@ -740,7 +763,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                                               0, 0, 0);
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const int b = 4 * t + q;
+                    const int b = bidx(t);
                     const float gh = net ? s0[t] * wa0 : s0[t] * wa0 + s1[t] * wa1;
                     const float hv = ha[t];
                     const float dz = gh * (1.0f - hv * hv);
