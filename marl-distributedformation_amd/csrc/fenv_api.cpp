@@ -113,10 +113,19 @@ struct fenv {
     int64_t total = 0;  // formations in the whole (unsharded) batch
     int64_t A = 0;
     fenvk::DevState s{};
-    float *pend = nullptr;   // device: px[A] py[A] gx[F] gy[F] of the next MT reset event
-    float *hpend = nullptr;  // pinned host staging for `pend`
-    hipEvent_t pend_ev = nullptr;
-    bool pend_ev_recorded = false;
+    // MT19937 reset sets, double-buffered: slot k of `pend` (device) and of `hpend` (pinned,
+    // coherent host memory, read by the staging kernel through `hpend_dev`) each hold one set,
+    // px[A] py[A] gx[F] gy[F].  `rd` is the slot the next reset event reads; a refill writes the
+    // other slot, so it never touches a set a queued launch may still read, and the host only
+    // rewrites a host slot whose copy (two refills back) has finished.
+    float *pend = nullptr;
+    float *hpend = nullptr;
+    float *hpend_dev = nullptr;
+    hipEvent_t pend_ev[2] = {nullptr, nullptr};  // staging copy of slot k done
+    hipEvent_t used_ev[2] = {nullptr, nullptr};  // the launch that consumed slot k is done
+    bool pend_ev_recorded[2] = {false, false};
+    bool used_ev_recorded[2] = {false, false};
+    int rd = 1;
     float *term = nullptr;   // device: terminal (px, py, gx, gy)[A] of the latest done step
     bool term_valid = false; // last state-changing call was a step (t == 0 <=> reset by it)
     float *lv_scratch = nullptr;  // last values for GAE when the caller passes none
@@ -125,33 +134,44 @@ struct fenv {
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
 
     size_t pend_floats() const { return (size_t)(2 * A + 2 * c.F); }
+    size_t pend_stride() const { return (pend_floats() + 63) & ~(size_t)63; }  // 256-B slots
     fenvk::DevPending pending() const {
-        return fenvk::DevPending{pend, reinterpret_cast<float4 *>(term), lf};
+        return fenvk::DevPending{pend ? pend + (size_t)rd * pend_stride() : nullptr,
+                                 reinterpret_cast<float4 *>(term), lf};
     }
 
-    // A launch that may read the staged set waits (on the device) for its latest refill, which
-    // may have been issued on another stream; refills are issued on the stream of the launch
-    // that consumed the previous set, so they never overtake a reader.
+    // A launch that may read the staged set waits (on the device) for its refill, which may have
+    // been issued on another stream.
     int wait_pending(hipStream_t st) {
-        if (c.reset_mode == FENV_RESET_MT19937 && pend_ev_recorded)
-            FENV_HIP(hipStreamWaitEvent(st, pend_ev, 0));
+        if (c.reset_mode == FENV_RESET_MT19937 && pend_ev_recorded[rd])
+            FENV_HIP(hipStreamWaitEvent(st, pend_ev[rd], 0));
         return FENV_OK;
     }
 
-    // Draw the next reset set of the global stream; keep this shard's part; stage it to HBM.
+    // Called right after the launch that consumed slot rd was queued on `st`: draw the next
+    // reset set of the global stream, keep this shard's part, stage it into the other slot.
     int gen_pending(hipStream_t st) {
         if (c.reset_mode != FENV_RESET_MT19937) return FENV_OK;
-        if (pend_ev_recorded) FENV_HIP(hipEventSynchronize(pend_ev));  // staging buffer free
+        const int w = rd ^ 1;
+        if (pend_ev_recorded[rd]) {  // slot rd now has a queued reader on st
+            FENV_HIP(hipEventRecord(used_ev[rd], st));
+            used_ev_recorded[rd] = true;
+        }
+        if (pend_ev_recorded[w]) FENV_HIP(hipEventSynchronize(pend_ev[w]));  // host slot free
+        const size_t off = (size_t)w * pend_stride();
         const uint64_t per = 2ull * (uint64_t)c.N + 2ull;
         mt.discard(per * (uint64_t)c.f0);
-        float *px = hpend, *py = hpend + A, *gx = hpend + 2 * A, *gy = hpend + 2 * A + c.F;
+        float *hp = hpend + off;
+        float *px = hp, *py = hp + A, *gx = hp + 2 * A, *gy = hp + 2 * A + c.F;
         for (int64_t f = 0; f < c.F; ++f)
             draw_formation(mt, c.N, px + f * c.N, py + f * c.N, gx[f], gy[f]);
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
-        FENV_HIP(hipMemcpyAsync(pend, hpend, pend_floats() * sizeof(float), hipMemcpyHostToDevice,
-                                st));
-        FENV_HIP(hipEventRecord(pend_ev, st));
-        pend_ev_recorded = true;
+        // the slot's previous reader (the launch that consumed it, on whatever stream) first
+        if (used_ev_recorded[w]) FENV_HIP(hipStreamWaitEvent(st, used_ev[w], 0));
+        FENV_HIP(fenvk::launch_stage_copy(pend + off, hpend_dev + off, (int64_t)pend_floats(), st));
+        FENV_HIP(hipEventRecord(pend_ev[w], st));
+        pend_ev_recorded[w] = true;
+        rd = w;
         return FENV_OK;
     }
 
@@ -258,12 +278,18 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(exchange scratch) failed"));
     }
     if (reset_mode == FENV_RESET_MT19937) {
-        he = hipMalloc(&e->pend, e->pend_floats() * sizeof(float));
+        const size_t pb = 2 * e->pend_stride() * sizeof(float);
+        he = hipMalloc(&e->pend, pb);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
-        he = hipHostMalloc(&e->hpend, e->pend_floats() * sizeof(float), hipHostMallocDefault);
+        he = hipHostMalloc(&e->hpend, pb, hipHostMallocMapped | hipHostMallocCoherent);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipHostMalloc(pending) failed"));
-        he = hipEventCreateWithFlags(&e->pend_ev, hipEventDisableTiming);
-        if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipEventCreate failed"));
+        he = hipHostGetDevicePointer(reinterpret_cast<void **>(&e->hpend_dev), e->hpend, 0);
+        if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipHostGetDevicePointer failed"));
+        for (int k = 0; k < 2; ++k) {
+            he = hipEventCreateWithFlags(&e->pend_ev[k], hipEventDisableTiming);
+            if (he == hipSuccess) he = hipEventCreateWithFlags(&e->used_ev[k], hipEventDisableTiming);
+            if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipEventCreate failed"));
+        }
     }
     // FormationEnv ctor: every FormationSimulator.__init__ calls reset() (simulate.py:61).
     int rc = e->gen_pending(nullptr);
@@ -288,11 +314,15 @@ int fenv_destroy(fenv_t *e) {
     const bool have_prev = hipGetDevice(&prev) == hipSuccess;
     (void)hipSetDevice(e->device);
     drain_graveyard();
-    if (e->pend_ev_recorded) (void)hipEventSynchronize(e->pend_ev);
+    for (int k = 0; k < 2; ++k)
+        if (e->pend_ev_recorded[k]) (void)hipEventSynchronize(e->pend_ev[k]);
     free_dev(e->device, e->s.px);
     free_dev(e->device, e->pend);
     free_host(e->device, e->hpend);
-    if (e->pend_ev) (void)hipEventDestroy(e->pend_ev);
+    for (int k = 0; k < 2; ++k) {
+        if (e->pend_ev[k]) (void)hipEventDestroy(e->pend_ev[k]);
+        if (e->used_ev[k]) (void)hipEventDestroy(e->used_ev[k]);
+    }
     free_dev(e->device, e->lv_scratch);
     free_dev(e->device, e->term);
     free_dev(e->device, e->lf);

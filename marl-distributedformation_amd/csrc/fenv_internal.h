@@ -91,6 +91,7 @@ hipError_t launch_reset_observe_large(const Consts &c, const DevState &s, const 
                                       int32_t D, bool do_reset, float *obs, hipStream_t st);
 hipError_t launch_metrics_large(const Consts &c, const DevState &s, const DevPending &p,
                                 bool terminal, const float *rew, float *out, hipStream_t st);
+hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, hipStream_t st);
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st);
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,

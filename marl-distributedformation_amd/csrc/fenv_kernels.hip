@@ -998,6 +998,29 @@ hipError_t launch_reduce_partials(const float *partial, int64_t count, double *o
     return hipGetLastError();
 }
 
+// Staged MT19937 reset set: pinned host buffer -> HBM, as a kernel on the launch stream (the
+// refill is then ordered with the rollout kernels by the stream's in-order AQL queue alone; the
+// host buffer is read over the bus through its mapped device address).  n floats, any n.
+__global__ __launch_bounds__(256) void k_stage_copy(float *__restrict__ dst,
+                                                    const float *__restrict__ src, int64_t n) {
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+        d4[i] = s4[i];
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n - 4 * n4) dst[4 * n4 + t] = src[4 * n4 + t];
+}
+
+hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, hipStream_t st) {
+    int64_t blocks = (n / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,
                            hipStream_t st) {
     int64_t blocks = (n + 255) / 256;
