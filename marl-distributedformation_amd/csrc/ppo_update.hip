@@ -80,7 +80,9 @@ static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
               "parameter image too small for D = 8");
 
 // per-sample scalar slots
-enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV, sMU0, sMU1, sVAL };
+enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV, sMU0, sMU1, sVAL,
+       sPL, sCF, sGL0, sGL1, sVLS };  // the last five: per-sample loss terms (FENV_PPO_LOSS_SPREAD)
+constexpr int kEnt = 56;              // R slot: the entropy (FENV_PPO_LOSS_SPREAD)
 
 struct PPOArgs {
     float *params, *exp_avg, *exp_avg_sq, *step;
@@ -418,11 +420,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_SEP 1
 #endif
     constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
+#ifndef FENV_PPO_LOSS_SPREAD
+#define FENV_PPO_LOSS_SPREAD 1
+#endif
+    // split launch: the loss wave writes per-sample terms; waves 1-3 take the sums afterwards
+    constexpr bool kSpread = SPLIT && FENV_PPO_LOSS_SPREAD && !FENV_PPO_LOSS_PRE;
+    const int stat_tid = kSpread ? 64 : 0;  // the thread accumulating the loss statistics
 #ifndef FENV_PPO_HG_VEC
 #define FENV_PPO_HG_VEC 1
 #endif
 #ifndef FENV_PPO_LS_EARLY
-#define FENV_PPO_LS_EARLY 1
+#define FENV_PPO_LS_EARLY 0
 #endif
     constexpr bool kLE = FENV_PPO_LS_EARLY && !FENV_PPO_LOSS_PRE;
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_EARLY_X 0
 #endif
 #ifndef FENV_PPO_ADAM_FMA
-#define FENV_PPO_ADAM_FMA 0
+#define FENV_PPO_ADAM_FMA 1
 #endif
     float a_coef = 0.f, a_ss = 0.f, a_ib = 0.f;  // clip coef, step size, 1/sqrt(bc2)
     float gq[SPLIT ? KP : 1], wq[SPLIT ? KP : 1];
@@ -633,7 +641,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 (void)var0;
                 (void)var1;
 #else
-                if (!kLE) loss_consts();
+                if (!kLE && (!kSpread || do_pi)) loss_consts();
                 const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
                 const float iv0 = lc_iv0, iv1 = lc_iv1;
                 (void)lc_var0;
@@ -641,7 +649,54 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
-                if (on) {
+                if constexpr (kSpread) {
+                    // split launch: this block's terms only; the sums over the samples are taken
+                    // by waves 1-3 at the start of the next phase (per-sample values in S)
+                    const float kLogSqrt2Pi = 0.918938533204672742f;
+                    if (do_pi) {
+                        if (on) {
+                            const float mu0 = S[sMU0 * kPB + lane], mu1 = S[sMU1 * kPB + lane];
+                            const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
+                            const float d0 = a0 - mu0, d1 = a1 - mu1;
+                            const float lp = (-(d0 * d0) * i2v0 - lsd0 - kLogSqrt2Pi) +
+                                             (-(d1 * d1) * i2v1 - lsd1 - kLogSqrt2Pi);
+                            const float ratio = expf(lp - S[sOLP * kPB + lane]);
+                            const float an = S[sADV * kPB + lane];
+                            const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
+                            const float rc = ratio < lo ? lo : (ratio > hi ? hi : ratio);
+                            const float l1 = an * ratio, l2 = an * rc;
+                            pl = l1 < l2 ? l1 : l2;
+                            cf = fabsf(ratio - 1.0f) > hp.clip_range ? 1.0f : 0.0f;
+                            const float g1 = l1 < l2 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f);
+                            const float g2 = l2 < l1 ? 1.0f : (l1 == l2 ? 0.5f : 0.0f);
+                            const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+                            const float dratio = -(g1 * an + g2 * an * inside) * invB;
+                            const float dlp = dratio * ratio;
+                            gmu0 = dlp * (d0 * iv0);
+                            gmu1 = dlp * (d1 * iv1);
+                            gls0 = dlp * ((d0 * d0) * iv0 - 1.0f);
+                            gls1 = dlp * ((d1 * d1) * iv1 - 1.0f);
+                        }
+                        S[sGMU0 * kPB + lane] = gmu0;
+                        S[sGMU1 * kPB + lane] = gmu1;
+                        S[sPL * kPB + lane] = pl;
+                        S[sCF * kPB + lane] = cf;
+                        S[sGL0 * kPB + lane] = gls0;
+                        S[sGL1 * kPB + lane] = gls1;
+                        if (lane == 0) {
+                            const float kHalfLog2PiE = 1.41893853320467274f;  // 0.5 + 0.5 log(2 pi)
+                            R[kEnt] = (kHalfLog2PiE + lsd0) + (kHalfLog2PiE + lsd1);
+                        }
+                    } else {
+                        if (on) {
+                            const float rr = S[sRET * kPB + lane] - S[sVAL * kPB + lane];
+                            vl = rr * rr;
+                            gv = hp.vf_coef * (-2.0f * rr) * invB;
+                        }
+                        S[sGV * kPB + lane] = gv;
+                        S[sVLS * kPB + lane] = vl;
+                    }
+                } else if (on) {
                     const float mu0 = S[sMU0 * kPB + lane], mu1 = S[sMU1 * kPB + lane];
                     const float val = S[sVAL * kPB + lane];
                     const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
@@ -671,6 +726,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     gls0 = dlp * ((d0 * d0) * iv0 - 1.0f);
                     gls1 = dlp * ((d1 * d1) * iv1 - 1.0f);
                 }
+                if constexpr (!kSpread) {
                 if (do_pi) {
                     S[sGMU0 * kPB + lane] = gmu0;
                     S[sGMU1 * kPB + lane] = gmu1;
@@ -707,9 +763,53 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         gss += sgv * sgv;
                     }
                 }
+                }  // !kSpread
             }
             __syncthreads();
             FENV_PPO_PHASE(3);
+            // kSpread: the loss sums, one or two per wave of waves 1-3 (wave 0 just ran the loss);
+            // their outputs are only read from the norm phase on
+            if constexpr (kSpread) {
+                if (net_b == 0) {
+                    if (wl == 1) {
+                        const float spl = wsum(S[sPL * kPB + lane]), scf = wsum(S[sCF * kPB + lane]);
+                        if (lane == 0) {
+                            st_pl += (double)(-spl * invB);
+                            if (!GRAD || g.ent_once) st_el += (double)(-R[kEnt]);
+                            st_cf += (double)(scf * invB);
+                        }
+                    } else if (wl == 2) {
+                        // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef; gradient mode: the
+                        // entropy term once over the ranks (ent_once)
+                        const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
+                        const float g0 = wsum(S[sGL0 * kPB + lane]) - ec;
+                        const float g1 = wsum(S[sGL1 * kPB + lane]) - ec;
+                        if (lane == 0) {
+                            G[lx(L.logstd)] = g0;
+                            G[lx(L.logstd + 1)] = g1;
+                            gss += g0 * g0 + g1 * g1;
+                        }
+                    } else if (wl == 3) {
+                        const float m0 = wsum(S[sGMU0 * kPB + lane]), m1 = wsum(S[sGMU1 * kPB + lane]);
+                        if (lane == 0) {
+                            G[lx(L.actb)] = m0;
+                            G[lx(L.actb + 1)] = m1;
+                            gss += m0 * m0 + m1 * m1;
+                        }
+                    }
+                } else {
+                    if (wl == 1) {
+                        const float svl = wsum(S[sVLS * kPB + lane]);
+                        if (lane == 0) st_vl += (double)(svl * invB);
+                    } else if (wl == 2) {
+                        const float sgv = wsum(S[sGV * kPB + lane]);
+                        if (lane == 0) {
+                            G[lx(L.valb)] = sgv;
+                            gss += sgv * sgv;
+                        }
+                    }
+                }
+            }
             // ---- head weight gradients on v_mfma_f32_16x16x4f32 (wave w = net w>>2, hidden rows
             // 16(w&3)..+15, columns gmu0/gmu1 resp. gv; K = 64 samples as 16 MFMAs), then
             // dL/dz2 in place over the SAME H2 columns (only this wave reads or writes them in
@@ -1069,8 +1169,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
         }
     }
-    if (tid == 0 && net_b == 0) {
-        if (!GRAD) g.step[0] = step;
+    if (tid == 0 && net_b == 0 && !GRAD) g.step[0] = step;
+    if (tid == stat_tid && net_b == 0) {
         atomicAdd(g.stats + 0, st_pl);  // atomic: the other block may mark a lost exchange
         if (!SPLIT) g.stats[1] += st_vl;
         g.stats[2] += st_el;
@@ -1080,7 +1180,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     if (tid == 0 && net_b == (FENV_PPO_PROFILE == 2 ? 1 : 0))
         for (int q = 0; q < 11; ++q) g.stats[4 + q] += prof[q];
 #endif
-    if (SPLIT && tid == 0 && net_b == 1) g.stats[1] += st_vl;
+    if (SPLIT && tid == stat_tid && net_b == 1) g.stats[1] += st_vl;
     // split: a norm exchange that timed out leaves NaN parameters; say so in the stats, which the
     // host checks (ppo.py).  Atomic adds, so the mark survives in whichever order the two blocks
     // write: NaN policy-loss sum, and a clip-fraction sum far below zero (a lost partner, not
