@@ -73,7 +73,8 @@ constexpr int oPH1 = oPO + kPB * 9;           // [2][kPB][kRow] layer-1 tanh, th
 constexpr int oPH2 = oPH1 + 2 * kPB * kRow;   // [2][kPB][kRow] layer-2 tanh, then dL/dz2
 constexpr int oPS = oPH2 + 2 * kPB * kRow;    // [16][kPB] per-sample scalars
 constexpr int oPR = oPS + 16 * kPB;           // [64] reduction scratch
-constexpr int kPPOLds = oPR + 64;
+constexpr int oPB1 = oPR + 64;                // [2][64] b1-gradient partial sums (FENV_PPO_B1_PART)
+constexpr int kPPOLds = oPB1 + 2 * kHid;
 constexpr size_t kPPOLdsBytes = (size_t)kPPOLds * sizeof(float);
 static_assert(kPPOLdsBytes <= 160 * 1024, "fused PPO update exceeds the 160 KiB LDS of a CU");
 static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     const int net_b = SPLIT ? (int)(blockIdx.x >> 3) : 0;  // split: this block's network
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *W = sm + oPW, *G = sm + oPG, *O = sm + oPO, *H1 = sm + oPH1, *H2 = sm + oPH2;
-    float *S = sm + oPS, *R = sm + oPR;
+    float *S = sm + oPS, *R = sm + oPR, *B1P = sm + oPB1;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wl = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave of this block
     const int w = wl + (SPLIT ? 4 * net_b : 0);               // wave index of the unsplit kernel
@@ -426,6 +427,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     // split launch: the loss wave writes per-sample terms; waves 1-3 take the sums afterwards
     constexpr bool kSpread = SPLIT && FENV_PPO_LOSS_SPREAD && !FENV_PPO_LOSS_PRE;
     const int stat_tid = kSpread ? 64 : 0;  // the thread accumulating the loss statistics
+#ifndef FENV_PPO_B2_HG
+#define FENV_PPO_B2_HG 1  // split: the b2 gradient summed by the head-gradient phase's lanes
+#endif
+#ifndef FENV_PPO_B1_PART
+#define FENV_PPO_B1_PART 1  // split: b1-gradient partial sums from the dL/dz1 writers
+#endif
+    constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
+    constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
+#ifndef FENV_PPO_HEADS_K16
+#define FENV_PPO_HEADS_K16 1
+#endif
 #ifndef FENV_PPO_HG_VEC
 #define FENV_PPO_HG_VEC 1
 #endif
@@ -435,6 +447,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     constexpr bool kLE = FENV_PPO_LS_EARLY && !FENV_PPO_LOSS_PRE;
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
+#ifndef FENV_PPO_ADAM_PRE
+#define FENV_PPO_ADAM_PRE 1
+#endif
+    constexpr bool kAP = SPLIT && !GRAD && FENV_PPO_ADAM_PRE;
 #ifndef FENV_PPO_EARLY_X
 #define FENV_PPO_EARLY_X 0
 #endif
@@ -448,6 +464,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         if (p < P) {
             const int ix = SPLIT ? lp[q] : lx(p);
             const float gr = (SPLIT ? gq[q] : G[ix]) * a_coef;
+            if constexpr (kAP) {  // m, v already hold beta1 m, beta2 v (adam_pre)
+                m[q] = __builtin_fmaf(1.0f - hp.beta1, gr, m[q]);
+                v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q]);
+                const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v[q]), a_ib, hp.eps);
+                W[ix] = __builtin_fmaf(-a_ss, m[q] * __builtin_amdgcn_rcpf(den), wq[q]);
+                return;
+            }
 #if FENV_PPO_ADAM_FMA
             m[q] = __builtin_fmaf(1.0f - hp.beta1, gr - m[q], m[q]);
             v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q] * hp.beta2);
@@ -463,6 +486,20 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             const float wn = (SPLIT ? wq[q] : W[ix]) - a_ss * (m[q] * __builtin_amdgcn_rcpf(den));
 #endif
             W[ix] = wn;
+        }
+    };
+    // kAP: the coefficient-free half of Adam (decayed moments, bias corrections) while the norm
+    // exchange is in flight
+    auto adam_pre = [&]() {
+        step += 1.0f;
+        const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
+        const float bc2 = 1.0f - exp2f(step * lb2);
+        a_ss = hp.lr / bc1;
+        a_ib = 1.0f / __builtin_sqrtf(bc2);
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+            m[q] = hp.beta1 * m[q];
+            v[q] = hp.beta2 * v[q];
         }
     };
     // the deferred slots of the previous minibatch's Adam step (kAS)
@@ -603,11 +640,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int hw = net ? L.valW : L.actW + (c & 1) * kHid;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                 if constexpr (SPLIT) {  // operands read up front, branch-free (see head grads)
+                    // K-step s4 of lane group q: hidden unit 16 q + s4 (FENV_PPO_HEADS_K16: the
+                    // 64 lanes of a read hit 64 banks) or 4 s4 + q
                     float av[16], wv[16];
 #pragma unroll
                     for (int s4 = 0; s4 < 16; ++s4) {
-                        av[s4] = a[4 * s4];
-                        wv[s4] = W[lx(hw + 4 * s4 + q)];
+                        const int kk = FENV_PPO_HEADS_K16 ? 16 * q + s4 : 4 * s4 + q;
+                        av[s4] = a[kk - q];
+                        wv[s4] = W[lx(hw + kk)];
                     }
 #pragma unroll
                     for (int s4 = 0; s4 < 16; ++s4)
@@ -861,13 +901,24 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 for (int t = 0; t < 16; ++t)
                     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[t], c < ncol ? sb[t] : 0.0f, acc,
                                                               0, 0, 0);
+                float b2p = 0.0f;  // kB2: this lane's part of the b2 gradient of column k
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const int b = bidx(t);
                     const float gh = net ? s0[t] * wa0 : s0[t] * wa0 + s1[t] * wa1;
                     const float hv = ha[t];
                     const float dz = gh * (1.0f - hv * hv);
-                    hcol[b * kRow + c] = b < B ? dz : 0.0f;
+                    const float dzb = b < B ? dz : 0.0f;
+                    hcol[b * kRow + c] = dzb;
+                    if (kB2) b2p += dzb;
+                }
+                if constexpr (kB2) {  // b2 gradient = column sum of dL/dz2 (the 4 lane groups)
+                    b2p += __shfl_xor(b2p, 16, 64);
+                    b2p += __shfl_xor(b2p, 32, 64);
+                    if (q == 0) {
+                        G[lx((net ? L.vf2b : L.pi2b) + k)] = b2p;
+                        gss = __builtin_fmaf(b2p, b2p, gss);
+                    }
                 }
                 if (c < ncol) {
                     const int hw = net ? L.valW : L.actW + c * kHid;
@@ -977,7 +1028,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     Gr[rho(r, h) * kRow] = gw[r];
                     gss = __builtin_fmaf(gw[r], gw[r], gss);
                 }
-                if (tid < (SPLIT ? kHid : 2 * kHid)) {
+                if (!kB2 && tid < (SPLIT ? kHid : 2 * kHid)) {
                     const int bn = SPLIT ? net_b : tid >> 6, j = tid & 63;
                     const float *z2 = H2 + bn * kPB * kRow + j;
                     const float acc = col_sum(z2, B);
@@ -990,10 +1041,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 FENV_PPO_PHASE(6);
                 const float *H1r = H1 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
                 float *Z1w = H1 + ((kZ1S ? zb : net) * kPB + 32 * mt) * kRow + 32 * nt + c;
+                float b1p = 0.0f;  // kB1: this lane's part of the b1 gradient of its column
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float hv = H1r[rho(r, h) * kRow];
-                    Z1w[rho(r, h) * kRow] = dz[r] * (1.0f - hv * hv);
+                    const float z1 = dz[r] * (1.0f - hv * hv);
+                    Z1w[rho(r, h) * kRow] = z1;
+                    if (kB1) b1p += z1;
+                }
+                if constexpr (kB1) {  // rows of this tile (both lane halves); the other row tile's
+                    b1p += __shfl_xor(b1p, 32, 64);  // wave adds its part in the W1 phase
+                    if (h == 0) B1P[mt * kHid + 32 * nt + c] = b1p;
                 }
             }
             __syncthreads();
@@ -1039,7 +1097,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if (tid < (SPLIT ? kHid : 2 * kHid)) {
                 const int net = SPLIT ? net_b : tid >> 6, j = tid & 63;
                 const float *z1 = H1 + (kZ1S ? (net ^ 1) : net) * kPB * kRow + j;
-                const float acc = col_sum(z1, B);
+                const float acc = kB1 ? B1P[j] + B1P[kHid + j] : col_sum(z1, B);
                 G[lx((net ? L.vf0b : L.pi0b) + j)] = acc;
                 gss = __builtin_fmaf(acc, acc, gss);
             }
@@ -1108,6 +1166,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                      net_b == 0 ? adv_nx : ps[3]);
                     }
                 }
+                if constexpr (kAP) adam_pre();
                 if (tid == 0) {
                     // after one timed-out wait the partner is taken as lost for good: no further
                     // waits, so a broken launch ends in milliseconds, not one timeout per
@@ -1130,12 +1189,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             float coef = hp.max_grad_norm / (norm + 1e-6f);
             coef = coef < 1.0f ? coef : 1.0f;
             // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
-            step += 1.0f;
-            const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
-            const float bc2 = 1.0f - exp2f(step * lb2);
             a_coef = coef;
-            a_ss = hp.lr / bc1;
-            a_ib = 1.0f / __builtin_sqrtf(bc2);
+            if constexpr (!kAP) {
+                step += 1.0f;
+                const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
+                const float bc2 = 1.0f - exp2f(step * lb2);
+                a_ss = hp.lr / bc1;
+                a_ib = 1.0f / __builtin_sqrtf(bc2);
+            }
             // kAS: slots 0..kKA-1 (layer 1) now, the rest in the next minibatch's layer-1 phase
 #pragma unroll
             for (int q = 0; q < kKA; ++q) adam_slot(q);

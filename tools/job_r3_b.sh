@@ -8,4 +8,4 @@ for v in nprof1 prof1; do
   echo "== PPO phase profile $v"
   FENV_LIB_OVERRIDE=$PWD/build_variants/libfenv_$v.so timeout -k 10 100 python -u tools/ppo_phase_profile.py 2>&1 | grep -v amdgpu.ids || exit $?
 done
-PAIRS=${PAIRS:-2} VARIANTS="${PPO_VARIANTS:-old as0 sp0 fma0 hg0 lp1}" timeout -k 10 700 bash tools/ppo_variant_ab.sh 2>&1 | grep -v amdgpu.ids | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//; s/'samples_per_s'.*//"
+PAIRS=${PAIRS:-2} VARIANTS="${PPO_VARIANTS:-old as0 sp0 ap0 b20 b10 hk0}" timeout -k 10 700 bash tools/ppo_variant_ab.sh 2>&1 | grep -v amdgpu.ids | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//; s/'samples_per_s'.*//"
