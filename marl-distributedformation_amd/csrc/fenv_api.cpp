@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <random>
 #include <string>
@@ -83,6 +84,50 @@ void free_host(int32_t device, void *p) {
         std::lock_guard<std::mutex> lk(graveyard().mu);
         graveyard().host.emplace_back(device, p);
     }
+}
+// Pinned staging buffers of the MT19937 reset sets are pooled for the process and never freed:
+// a destroyed env's buffer goes back to the pool and the next env takes it (smallest that fits),
+// so host staging addresses are never released and re-mapped while the process runs.
+struct PinnedPool {
+    std::mutex mu;
+    std::multimap<size_t, std::pair<float *, float *>> free;  // bytes -> (host, device address)
+};
+PinnedPool &pinned_pool() {
+    static PinnedPool *p = new PinnedPool();  // never destroyed: usable from atexit / finalizers
+    return *p;
+}
+hipError_t pinned_take(size_t bytes, float **host, float **dev) {
+    {
+        std::lock_guard<std::mutex> lk(pinned_pool().mu);
+        auto it = pinned_pool().free.lower_bound(bytes);
+        if (it != pinned_pool().free.end()) {
+            *host = it->second.first;
+            *dev = it->second.second;
+            pinned_pool().free.erase(it);
+            return hipSuccess;
+        }
+    }
+    void *h = nullptr;
+    hipError_t he = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent |
+                                                 hipHostMallocPortable);
+    if (he != hipSuccess) return he;
+    void *d = nullptr;
+    he = hipHostGetDevicePointer(&d, h, 0);
+    if (he != hipSuccess) {
+        (void)hipHostFree(h);
+        return he;
+    }
+    // the pool entry records its capacity in the word before the buffer
+    *reinterpret_cast<size_t *>(h) = bytes;
+    *host = reinterpret_cast<float *>(reinterpret_cast<char *>(h) + 256);
+    *dev = reinterpret_cast<float *>(reinterpret_cast<char *>(d) + 256);
+    return hipSuccess;
+}
+void pinned_give(float *host, float *dev) {
+    if (!host) return;
+    const size_t bytes = *reinterpret_cast<size_t *>(reinterpret_cast<char *>(host) - 256);
+    std::lock_guard<std::mutex> lk(pinned_pool().mu);
+    pinned_pool().free.emplace(bytes, std::make_pair(host, dev));
 }
 // Retry the parked frees (each is parked again if a capture is still under way).
 void drain_graveyard() {
@@ -281,10 +326,8 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
         const size_t pb = 2 * e->pend_stride() * sizeof(float);
         he = hipMalloc(&e->pend, pb);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
-        he = hipHostMalloc(&e->hpend, pb, hipHostMallocMapped | hipHostMallocCoherent);
+        he = pinned_take(pb + 256, &e->hpend, &e->hpend_dev);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipHostMalloc(pending) failed"));
-        he = hipHostGetDevicePointer(reinterpret_cast<void **>(&e->hpend_dev), e->hpend, 0);
-        if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipHostGetDevicePointer failed"));
         for (int k = 0; k < 2; ++k) {
             he = hipEventCreateWithFlags(&e->pend_ev[k], hipEventDisableTiming);
             if (he == hipSuccess) he = hipEventCreateWithFlags(&e->used_ev[k], hipEventDisableTiming);
@@ -318,7 +361,7 @@ int fenv_destroy(fenv_t *e) {
         if (e->pend_ev_recorded[k]) (void)hipEventSynchronize(e->pend_ev[k]);
     free_dev(e->device, e->s.px);
     free_dev(e->device, e->pend);
-    free_host(e->device, e->hpend);
+    pinned_give(e->hpend, e->hpend_dev);
     for (int k = 0; k < 2; ++k) {
         if (e->pend_ev[k]) (void)hipEventDestroy(e->pend_ev[k]);
         if (e->used_ev[k]) (void)hipEventDestroy(e->used_ev[k]);
