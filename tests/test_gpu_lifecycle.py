@@ -169,3 +169,40 @@ def test_view_touches_only_its_formation(venv):
     assert torch.equal(env.metrics_range(a, b, rew[a * N:(a + b) * N]), env.metrics(rew)[a:a + b])
     with pytest.raises(IndexError):
         env.metrics_range(F - 1, 2)
+
+
+def test_mt_reset_staging_across_streams_and_churn(venv):
+    """The MT19937 reset sets are staged into two slots by a copy kernel on the launch stream
+    (DESIGN.md §9): many reset events inside one rollout call (the slot flips at each), launches
+    alternating between two streams (ordered only by stream waits), and staging buffers taken
+    back from the process pool by envs of other sizes -- every reward, obs and done bit-exact
+    against the C oracle."""
+    for F, N in ((40, 5), (3, 100), (700, 5)):  # pooled buffers of other sizes, then reused
+        e = make_env(venv, F, N, seed=F, max_steps=2)
+        e.rollout(torch.rand((7, F * N, 2), device=DEV) * 2 - 1)
+        e.release()
+    F, N = 500, 5
+    env = make_env(venv, F, N, seed=21, max_steps=2)
+    ref = COracleEnv(F, N, True, 21, max_steps=2)
+    assert np.array_equal(env.reset().view(np.uint32), ref.reset().view(np.uint32))
+    streams = [torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)]
+    prev = torch.cuda.current_stream(DEV)
+    k = 0
+    for call, T in enumerate((30, 5, 1, 9, 4, 13)):
+        st = streams[call % 2]
+        st.wait_stream(prev)
+        acts = np.stack([synth_actions(6, k + j, F * N, 1.1) for j in range(T)])
+        with torch.cuda.stream(st):
+            a = torch.from_numpy(acts).to(DEV, non_blocking=False)
+            obs, rew, done = env.rollout(a)
+        prev = st
+        st.synchronize()
+        obs, rew, done = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        for j in range(T):
+            ro, rr, rd, _ = ref.step(acts[j])
+            assert np.array_equal(rew[j].view(np.uint32), rr.view(np.uint32)), (call, k + j)
+            assert np.array_equal(obs[j].view(np.uint32), ro.view(np.uint32)), (call, k + j)
+            assert np.array_equal(done[j], rd), (call, k + j)
+        k += T
+    assert k > 40  # > 10 reset events at max_steps 2
+    env.release()
