@@ -435,6 +435,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
     constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
     constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
+#ifndef FENV_PPO_ACC2
+#define FENV_PPO_ACC2 1  // split: 16-step 16x16x4 MFMA chains as two interleaved accumulators
+#endif
+    constexpr bool kAcc2 = SPLIT && FENV_PPO_ACC2;
 #ifndef FENV_PPO_HEADS_K16
 #define FENV_PPO_HEADS_K16 1
 #endif
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
 #ifndef FENV_PPO_ADAM_PRE
-#define FENV_PPO_ADAM_PRE 1
+#define FENV_PPO_ADAM_PRE 0
 #endif
     constexpr bool kAP = SPLIT && !GRAD && FENV_PPO_ADAM_PRE;
 #ifndef FENV_PPO_EARLY_X
@@ -649,10 +653,18 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         av[s4] = a[kk - q];
                         wv[s4] = W[lx(hw + kk)];
                     }
+                    f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};  // kAcc2: two chains (even / odd steps)
 #pragma unroll
-                    for (int s4 = 0; s4 < 16; ++s4)
-                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], c < ncol ? wv[s4] : 0.0f,
-                                                                  acc, 0, 0, 0);
+                    for (int s4 = 0; s4 < 16; ++s4) {
+                        const float bw = c < ncol ? wv[s4] : 0.0f;
+                        if (kAcc2 && (s4 & 1))
+                            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bw, acc2, 0, 0, 0);
+                        else
+                            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bw, acc, 0, 0, 0);
+                    }
+                    if (kAcc2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[r] += acc2[r];
                 } else {
 #pragma unroll
                     for (int s4 = 0; s4 < 16; ++s4) {
@@ -897,10 +909,18 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
                 const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};  // kAcc2: two chains (even / odd steps)
 #pragma unroll
-                for (int t = 0; t < 16; ++t)
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[t], c < ncol ? sb[t] : 0.0f, acc,
-                                                              0, 0, 0);
+                for (int t = 0; t < 16; ++t) {
+                    const float bs_ = c < ncol ? sb[t] : 0.0f;
+                    if (kAcc2 && (t & 1))
+                        acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[t], bs_, acc2, 0, 0, 0);
+                    else
+                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[t], bs_, acc, 0, 0, 0);
+                }
+                if (kAcc2)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r] += acc2[r];
                 float b2p = 0.0f;  // kB2: this lane's part of the b2 gradient of column k
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
@@ -1072,10 +1092,18 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         zv[i] = Z1[b * kRow];
                         ov[i] = O[b * 9 + (c & 7)];
                     }
+                    f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};  // kAcc2: two chains (even / odd steps)
 #pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[i], c < 8 ? ov[i] : 0.0f, acc,
-                                                                  0, 0, 0);
+                    for (int i = 0; i < 16; ++i) {
+                        const float ob = c < 8 ? ov[i] : 0.0f;
+                        if (kAcc2 && (i & 1))
+                            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[i], ob, acc2, 0, 0, 0);
+                        else
+                            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(zv[i], ob, acc, 0, 0, 0);
+                    }
+                    if (kAcc2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[r] += acc2[r];
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
