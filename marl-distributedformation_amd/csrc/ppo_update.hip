@@ -435,6 +435,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
     constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
     constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
+#ifndef FENV_PPO_SCHED_PIN
+#define FENV_PPO_SCHED_PIN 1
+#endif
+#ifndef FENV_PPO_POST_FIRST
+#define FENV_PPO_POST_FIRST 1
+#endif
 #ifndef FENV_PPO_ACC2
 #define FENV_PPO_ACC2 1  // split: 16-step 16x16x4 MFMA chains as two interleaved accumulators
 #endif
@@ -595,6 +601,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     ra[j] = Ar[j];
                     rb[j] = Bc[j];
                 }
+                // FENV_PPO_SCHED_PIN: keep the ring's loads ahead of the MFMAs (the scheduler
+                // otherwise sinks them to their uses: an LDS round trip per MFMA pair)
+                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RL) {
 #pragma unroll
@@ -1016,12 +1025,16 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     rc[j] = pc[j];
                     rd[j] = pd[j * kRow];
                 }
+                // FENV_PPO_SCHED_PIN: loads ahead, and the two chains interleaved (the scheduler
+                // otherwise runs them one after the other with an LDS round trip per pair)
+                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RD) {
 #pragma unroll
                     for (int j = 0; j < RD; ++j) {
                         gw = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], gw, 0, 0, 0);
                         dz = __builtin_amdgcn_mfma_f32_32x32x2f32(rc[j], rd[j], dz, 0, 0, 0);
+                        if (FENV_PPO_SCHED_PIN == 2) __builtin_amdgcn_sched_barrier(0);
                         const int i = i0 + RD + j;
                         if (i < 32) {
                             ra[j] = pa[i * kRow];
@@ -1147,14 +1160,19 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             __syncthreads();
             FENV_PPO_PHASE(8);
             // split: this thread's gradient and parameter entries are read now, so the LDS
-            // reads overlap the norm exchange below
-            if constexpr (SPLIT) {
+            // reads overlap the norm exchange below (FENV_PPO_POST_FIRST: after the post -- LDS
+            // reads complete in order, so 40 reads queued ahead of the partial's own would
+            // delay the post)
+            auto read_gw = [&]() {
+                if constexpr (SPLIT) {
 #pragma unroll
-                for (int q = 0; q < KP; ++q) {
-                    gq[q] = G[lp[q]];
-                    wq[q] = W[lp[q]];
+                    for (int q = 0; q < KP; ++q) {
+                        gq[q] = G[lp[q]];
+                        wq[q] = W[lp[q]];
+                    }
                 }
-            }
+            };
+            if (!FENV_PPO_POST_FIRST) read_gw();
             float tot = 0.f;
             for (int q = 0; q < NT / 64; ++q) tot += R[q];
             if (SPLIT) {
@@ -1181,6 +1199,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
+                if (FENV_PPO_POST_FIRST) read_gw();
                 // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
                 // at this minibatch's gather) while the first load is in flight
                 if (net_b == 0 && wl == 0 && kmb + 1 < nmb) {
