@@ -448,6 +448,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #ifndef FENV_PPO_HEADS_K16
 #define FENV_PPO_HEADS_K16 1
 #endif
+#ifndef FENV_PPO_SUMS_W2
+#define FENV_PPO_SUMS_W2 1
+#endif
+    constexpr bool kSW2 = kSpread && FENV_PPO_SUMS_W2;
+#ifndef FENV_PPO_LS_EARLY
+#define FENV_PPO_LS_EARLY 0
+#endif
+#ifndef FENV_PPO_LS_L2
+#define FENV_PPO_LS_L2 1
+#endif
+    constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
 #ifndef FENV_PPO_HG_VEC
 #define FENV_PPO_HG_VEC 1
 #endif
@@ -560,12 +571,21 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int w1 = (net ? L.vf0W : L.pi0W) + j * D + q;
                 const float b0 = W[lx(w1)], b1 = W[lx(w1 + 4)];
                 const float bias = W[lx((net ? L.vf0b : L.pi0b) + j)];
+                // the 4 tiles' observation operands read up front (FENV_PPO_SCHED_PIN: kept
+                // ahead of the MFMAs, one LDS wait for the phase instead of one per tile)
+                float oa[4], ob[4];
 #pragma unroll
                 for (int bt = 0; bt < 4; ++bt) {
                     const float *o = O + (16 * bt + c) * 9 + q;
+                    oa[bt] = o[0];
+                    ob[bt] = o[4];
+                }
+                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int bt = 0; bt < 4; ++bt) {
                     f32x4 acc = {bias, bias, bias, bias};
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[0], b0, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[4], b1, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[bt], b0, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ob[bt], b1, acc, 0, 0, 0);
                     float *hr = H1 + (net * kPB + 16 * bt + 4 * q) * kRow + j;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) hr[r * kRow] = tanh_u(acc[r]);
@@ -581,6 +601,23 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(1);
+            // The loss's log_std-derived constants (FENV_PPO_LS_EARLY) are computed here, under the
+            // head MFMAs, by every wave (wave 0 keeps them for the loss phase): log_std was final
+            // at the layer-1 barrier, and the loss wave's chain then starts from the samples.
+            float lc_var0 = 0.f, lc_var1 = 0.f, lc_lsd0 = 0.f, lc_lsd1 = 0.f;
+            float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
+            auto loss_consts = [&]() {
+                const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
+                const float sd0 = expf(ls0), sd1 = expf(ls1);
+                lc_var0 = sd0 * sd0;
+                lc_var1 = sd1 * sd1;
+                lc_lsd0 = logf(sd0);  // torch: std.log()
+                lc_lsd1 = logf(sd1);
+                lc_i2v0 = 1.0f / (2.0f * lc_var0);
+                lc_i2v1 = 1.0f / (2.0f * lc_var1);
+                lc_iv0 = 1.0f / lc_var0;
+                lc_iv1 = 1.0f / lc_var1;
+            };
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
             // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
@@ -604,6 +641,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 // FENV_PPO_SCHED_PIN: keep the ring's loads ahead of the MFMAs (the scheduler
                 // otherwise sinks them to their uses: an LDS round trip per MFMA pair)
                 if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
+                // kLL2: the loss constants in the shadow of the 32 MFMAs (every wave, branch-free)
+                if (kLL2) loss_consts();
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RL) {
 #pragma unroll
@@ -628,23 +667,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
             // v_mfma_f32_16x16x4f32: wave w = net w>>2, samples 16(w&3)..+15, output columns 0..15
             // of which 2 (actor) / 1 (critic) are real; K = 64 hidden as 16 MFMAs
-            // The loss's log_std-derived constants (FENV_PPO_LS_EARLY) are computed here, under the
-            // head MFMAs, by every wave (wave 0 keeps them for the loss phase): log_std was final
-            // at the layer-1 barrier, and the loss wave's chain then starts from the samples.
-            float lc_var0 = 0.f, lc_var1 = 0.f, lc_lsd0 = 0.f, lc_lsd1 = 0.f;
-            float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
-            auto loss_consts = [&]() {
-                const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
-                const float sd0 = expf(ls0), sd1 = expf(ls1);
-                lc_var0 = sd0 * sd0;
-                lc_var1 = sd1 * sd1;
-                lc_lsd0 = logf(sd0);  // torch: std.log()
-                lc_lsd1 = logf(sd1);
-                lc_i2v0 = 1.0f / (2.0f * lc_var0);
-                lc_i2v1 = 1.0f / (2.0f * lc_var1);
-                lc_iv0 = 1.0f / lc_var0;
-                lc_iv1 = 1.0f / lc_var1;
-            };
             if (kLE) loss_consts();
             {
                 const int net = w >> 2, bt = w & 3, q = lane >> 4, c = lane & 15;
@@ -702,7 +724,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 (void)var0;
                 (void)var1;
 #else
-                if (!kLE && (!kSpread || do_pi)) loss_consts();
+                if (!kLE && !kLL2 && (!kSpread || do_pi)) loss_consts();
                 const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
                 const float iv0 = lc_iv0, iv1 = lc_iv1;
                 (void)lc_var0;
@@ -829,8 +851,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             __syncthreads();
             FENV_PPO_PHASE(3);
             // kSpread: the loss sums, one or two per wave of waves 1-3 (wave 0 just ran the loss);
-            // their outputs are only read from the norm phase on
-            if constexpr (kSpread) {
+            // their outputs are only read from the norm phase on (kSW2: taken in the shadow of
+            // the W2-gradient MFMAs instead, below)
+            if constexpr (kSpread && !kSW2) {
                 if (net_b == 0) {
                     if (wl == 1) {
                         const float spl = wsum(S[sPL * kPB + lane]), scf = wsum(S[sCF * kPB + lane]);
@@ -1028,6 +1051,16 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 // FENV_PPO_SCHED_PIN: loads ahead, and the two chains interleaved (the scheduler
                 // otherwise runs them one after the other with an LDS round trip per pair)
                 if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
+                // kSW2: this wave's two loss sums (slots by block and wave; wave 0 a dummy pair),
+                // branch-free so they issue between the MFMAs
+                float ls1 = 0.f, ls2 = 0.f;
+                if constexpr (kSW2) {
+                    constexpr int kT1[8] = {sPL, sPL, sGL0, sGMU0, sVLS, sVLS, sGV, sGV};
+                    constexpr int kT2[8] = {sPL, sCF, sGL1, sGMU1, sVLS, sVLS, sGV, sGV};
+                    const int ix = 4 * net_b + wl;
+                    ls1 = wsum(S[kT1[ix] * kPB + lane]);
+                    ls2 = wsum(S[kT2[ix] * kPB + lane]);
+                }
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RD) {
 #pragma unroll
@@ -1055,6 +1088,36 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                                              0, 0, 0);
                 }
 #endif
+                if constexpr (kSW2) {  // the lane-0 stores of the loss sums
+                    if (lane == 0) {
+                        if (net_b == 0) {
+                            if (wl == 1) {
+                                st_pl += (double)(-ls1 * invB);
+                                if (!GRAD || g.ent_once) st_el += (double)(-R[kEnt]);
+                                st_cf += (double)(ls2 * invB);
+                            } else if (wl == 2) {
+                                // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef; gradient
+                                // mode: the entropy term once over the ranks (ent_once)
+                                const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
+                                const float g0 = ls1 - ec, g1 = ls2 - ec;
+                                G[lx(L.logstd)] = g0;
+                                G[lx(L.logstd + 1)] = g1;
+                                gss += g0 * g0 + g1 * g1;
+                            } else if (wl == 3) {
+                                G[lx(L.actb)] = ls1;
+                                G[lx(L.actb + 1)] = ls2;
+                                gss += ls1 * ls1 + ls2 * ls2;
+                            }
+                        } else {
+                            if (wl == 1) {
+                                st_vl += (double)(ls1 * invB);
+                            } else if (wl == 2) {
+                                G[lx(L.valb)] = ls1;
+                                gss += ls1 * ls1;
+                            }
+                        }
+                    }
+                }
                 float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
