@@ -436,7 +436,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
     constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
 #ifndef FENV_PPO_SCHED_PIN
-#define FENV_PPO_SCHED_PIN 1
+#define FENV_PPO_SCHED_PIN 0
 #endif
 #ifndef FENV_PPO_POST_FIRST
 #define FENV_PPO_POST_FIRST 1

@@ -198,10 +198,13 @@ def test_fused_update_vs_torch_at_reference_config(mods):
     * chaotic: a 7,820-step trajectory of the clipped surrogate is not a smooth function of its
       inputs (a sample whose probability ratio sits at 1 +- clip_range, or a torch.min tie, flips
       its gradient for a last-bit difference, and Adam carries it forward).  torch is run from
-      the start parameters and from three copies moved by ONE ulp (every element up, every
-      element down, every other element up); 3x the largest torch-vs-torch spread is allowed,
-      per statistic (one perturbed run alone samples the tail of that spread too thinly: in
-      round 3 the fused max landed at 3.09x one such spread);
+      the start parameters, from three copies moved by ONE ulp (every element up, every
+      element down, every other element up), and on the CPU from the start parameters (its own
+      summation order at every step, as the kernel has); 3x the largest torch-vs-torch spread
+      is allowed, per statistic (one perturbed run alone samples that spread too thinly: in
+      round 3 the fused max landed at 3.09x one such spread, and the entropy loss, a mean of
+      log_std over the 7,820 steps, moves more under per-step rounding than under one start
+      perturbation);
     * coherent: the kernel's per-minibatch gradients agree with autograd to 2e-6 of their scale
       (test_ppo_grad_matches_autograd) and its Adam step to ~1 ulp, so with delta = 4e-6 relative
       per step, K = 7,820 steps of at most lr = 1e-3 move a parameter apart by at most
@@ -216,24 +219,65 @@ def test_fused_update_vs_torch_at_reference_config(mods):
                               use_fused=fused)
         with torch.no_grad():
             ppo.collector.collect()  # the rollout uses the unperturbed parameters
-            if ulp:
-                bits = ppo.policy.flat.view(torch.int32)
-                step = torch.ones_like(bits)
-                if ulp == "minus":
-                    step = -step
-                elif ulp == "alt":
-                    step[1::2] = 0
-                ppo.policy.flat.copy_((bits + step).view(torch.float32))
+            if ulp:  # one ulp up / down (nextafter: zeros move to the smallest subnormal)
+                f = ppo.policy.flat
+                up = torch.nextafter(f, torch.full_like(f, math.inf))
+                dn = torch.nextafter(f, torch.full_like(f, -math.inf))
+                if ulp == "plus":
+                    f.copy_(up)
+                elif ulp == "minus":
+                    f.copy_(dn)
+                else:  # every other element up
+                    f[0::2] = up[0::2]
+            samples = [t.detach().clone() for t in ppo._flat()]
         flat0 = ppo.policy.flat.clone()
         st = ppo.train()
         s = ppo.opt.state[ppo.param]
         assert float(s["step"]) == 7820
         env.release()
-        return flat0, ppo.policy.flat.clone(), st
+        return flat0, ppo.policy.flat.clone(), st, samples
 
-    a0, p0, s0 = run(False, False)
-    pert = [run(False, u)[1:] for u in ("plus", "minus", "alt")]
-    a1, p1, s1 = run(True, False)
+    def run_cpu(flat0, samples):
+        """The same update by torch on the CPU (another correct implementation: its own
+        summation orders at every step, non-capturable Adam) from the same parameters, samples
+        and permutations."""
+        c = mods["ppo"].PPOConfig()
+        obs, act, old_lp, adv, ret = (t.cpu() for t in samples)
+        n = obs.shape[0]
+        perms = mods["ppo"].epoch_permutations(
+            n, c.n_epochs, torch.Generator(device=DEV).manual_seed(3), DEV).cpu()
+        param = torch.nn.Parameter(flat0.cpu().clone())
+        opt = torch.optim.Adam([param], lr=c.learning_rate, eps=1e-5)
+        sums = torch.zeros(4, dtype=torch.float64)
+        steps = 0
+        for e in range(c.n_epochs):
+            for s0 in range(0, n, c.batch_size):
+                idx = perms[e, s0:s0 + c.batch_size]
+                values, log_prob, entropy = mods["ppo"].evaluate_actions(8, param, obs[idx],
+                                                                         act[idx])
+                a = adv[idx]
+                a = (a - a.mean()) / (a.std() + 1e-8)
+                ratio = torch.exp(log_prob - old_lp[idx])
+                l1, l2 = a * ratio, a * torch.clamp(ratio, 1 - c.clip_range, 1 + c.clip_range)
+                pl = -torch.min(l1, l2).mean()
+                vl = torch.nn.functional.mse_loss(ret[idx], values)
+                el = -torch.mean(entropy)
+                opt.zero_grad()
+                (pl + c.ent_coef * el + c.vf_coef * vl).backward()
+                torch.nn.utils.clip_grad_norm_([param], c.max_grad_norm)
+                opt.step()
+                cf = (torch.abs(ratio - 1) > c.clip_range).float().mean()
+                sums += torch.stack([pl.detach(), vl.detach(), el.detach(), cf]).double()
+                steps += 1
+        m = (sums / steps).tolist()
+        return param.detach().to(DEV), dict(policy_gradient_loss=m[0], value_loss=m[1],
+                                            entropy_loss=m[2], clip_fraction=m[3])
+
+    a0, p0, s0, smp = run(False, False)
+    pert = [run(False, u)[1:3] for u in ("plus", "minus", "alt")]
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    pert.append(run_cpu(a0, smp))
+    a1, p1, s1, _ = run(True, False)
     assert torch.equal(a0, a1)
     moved = (p0 - a0).abs()
     d_fused = (p1 - p0).abs()
@@ -244,7 +288,7 @@ def test_fused_update_vs_torch_at_reference_config(mods):
           f"{d_fused.max().item():.3g} median {d_fused.median().item():.3g}; |torch(1 ulp) - "
           f"torch| max {[round(d.max().item(), 7) for d in d_ulp]} median "
           f"{[float(f'{d.median().item():.3g}') for d in d_ulp]}")
-    print(f"losses torch {s0}\n       fused {s1}\n  torch 1ulp {[su for _, su in pert]}")
+    print(f"losses torch {s0}\n       fused {s1}\n  torch 1ulp / cpu {[su for _, su in pert]}")
     coherent = 7820 * 1e-3 * 4e-6
     assert moved.max().item() > 0.1  # the update did move the parameters
     assert d_fused.max().item() <= 3 * u_max + coherent
