@@ -42,6 +42,7 @@
 #include <atomic>
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <utility>
 
 #include "fenv.h"
@@ -129,6 +130,28 @@ __device__ __forceinline__ float tanh_u(float x) {
     return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
 #else
     return tanhf(x);
+#endif
+}
+
+// two at a time (FENV_PPO_TANH_PK): the same operations as float2, so the multiply / add /
+// fma steps issue as packed fp32
+#ifndef FENV_PPO_TANH_PK
+#define FENV_PPO_TANH_PK 1
+#endif
+__device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
+#if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK
+    using f2 = float __attribute__((ext_vector_type(2)));
+    const f2 x = {x0, x1};
+    const f2 t = x * 2.88539008177792681f;  // 2 log2(e)
+    const f2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    const f2 d = 1.0f + e;
+    const f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f2 y = 1.0f - 2.0f * r;
+    y0 = y.x;
+    y1 = y.y;
+#else
+    y0 = tanh_u(x0);
+    y1 = tanh_u(x1);
 #endif
 }
 
@@ -414,7 +437,19 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_ADAM_SPLIT 1
 #endif
     constexpr bool kAS = SPLIT && !GRAD && FENV_PPO_ADAM_SPLIT;
-    constexpr int kKA = kAS ? 3 : KP;  // ceil((64 D + 64) / 256) <= 3 for D <= 8
+#ifndef FENV_PPO_ADAM_PK
+#define FENV_PPO_ADAM_PK 1
+#endif
+#ifndef FENV_PPO_ADAM_PRE
+#define FENV_PPO_ADAM_PRE 0
+#endif
+#ifndef FENV_PPO_ADAM_FMA
+#define FENV_PPO_ADAM_FMA 1
+#endif
+    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && FENV_PPO_ADAM_FMA && !FENV_PPO_ADAM_PRE &&
+                         KP % 2 == 0;
+    // ceil((64 D + 64) / 256) <= 3 for D <= 8 (4 when packed: slot pairs)
+    constexpr int kKA = kAS ? (kPK ? 4 : 3) : KP;
     // dL/dz1 in the other network's H1 half (FENV_PPO_DZ1_SEP, split launch: each block owns
     // the whole LDS image but runs one network, so that half is free)
 #ifndef FENV_PPO_DZ1_SEP
@@ -509,6 +544,41 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             W[ix] = wn;
         }
     };
+    // Split launch, FENV_PPO_ADAM_PK: two slots per step as float2 arithmetic, so the compiler
+    // issues packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of fp32
+    // per VALU slot); same operations and roundings as two adam_slot calls (fused form)
+    using f2 = float __attribute__((ext_vector_type(2)));
+    auto adam_pair = [&](int q) {
+        const f2 g = {gq[q], gq[q + 1]};
+        const f2 gr = g * a_coef;
+        f2 mm = {m[q], m[q + 1]}, vv = {v[q], v[q + 1]};
+        const f2 c1 = 1.0f - hp.beta1, c2 = 1.0f - hp.beta2;
+        mm = __builtin_elementwise_fma(c1, gr - mm, mm);
+        vv = __builtin_elementwise_fma(c2, gr * gr, vv * hp.beta2);
+        const f2 sq = {__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
+        const f2 den = __builtin_elementwise_fma(sq, (f2)a_ib, (f2)hp.eps);
+        const f2 r = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        const f2 wv = {wq[q], wq[q + 1]};
+        const f2 wn = __builtin_elementwise_fma((f2)(-a_ss), mm * r, wv);
+        m[q] = mm.x;
+        m[q + 1] = mm.y;
+        v[q] = vv.x;
+        v[q + 1] = vv.y;
+        W[lp[q]] = wn.x;
+        W[lp[q + 1]] = wn.y;
+    };
+    // slots [q0, q1) of this thread's Adam step (pairs when kPK)
+    auto adam_slots = [&](auto q0c, auto q1c) {
+        constexpr int q0 = decltype(q0c)::value, q1 = decltype(q1c)::value;
+        if constexpr (kPK) {
+            static_assert(q0 % 2 == 0 && q1 % 2 == 0, "packed Adam runs slot pairs");
+#pragma unroll
+            for (int q = q0; q < q1; q += 2) adam_pair(q);
+        } else {
+#pragma unroll
+            for (int q = q0; q < q1; ++q) adam_slot(q);
+        }
+    };
     // kAP: the coefficient-free half of Adam (decayed moments, bias corrections) while the norm
     // exchange is in flight
     auto adam_pre = [&]() {
@@ -525,8 +595,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     };
     // the deferred slots of the previous minibatch's Adam step (kAS)
     auto adam_rest = [&]() {
-#pragma unroll
-        for (int q = kKA; q < KP; ++q) adam_slot(q);
+        adam_slots(std::integral_constant<int, kKA>{}, std::integral_constant<int, KP>{});
         // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
         if (FENV_PPO_LOSS_PRE && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
     };
@@ -588,7 +657,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ob[bt], b1, acc, 0, 0, 0);
                     float *hr = H1 + (net * kPB + 16 * bt + 4 * q) * kRow + j;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) hr[r * kRow] = tanh_u(acc[r]);
+                    for (int r = 0; r < 4; r += 2) {
+                        float y0, y1;
+                        tanh_u2(acc[r], acc[r + 1], y0, y1);
+                        hr[r * kRow] = y0;
+                        hr[(r + 1) * kRow] = y1;
+                    }
                 }
             };
             // kAS: the previous minibatch's deferred Adam slots in the same straight-line block
@@ -661,7 +735,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
                 float *Hr = H2 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) Hr[rho(r, h) * kRow] = tanh_u(acc[r]);
+                for (int r = 0; r < 16; r += 2) {
+                    float y0, y1;
+                    tanh_u2(acc[r], acc[r + 1], y0, y1);
+                    Hr[rho(r, h) * kRow] = y0;
+                    Hr[rho(r + 1, h) * kRow] = y1;
+                }
             }
             __syncthreads();
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
@@ -1308,8 +1387,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 a_ib = 1.0f / __builtin_sqrtf(bc2);
             }
             // kAS: slots 0..kKA-1 (layer 1) now, the rest in the next minibatch's layer-1 phase
-#pragma unroll
-            for (int q = 0; q < kKA; ++q) adam_slot(q);
+            adam_slots(std::integral_constant<int, 0>{}, std::integral_constant<int, kKA>{});
             // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
             if (!kAS && FENV_PPO_LOSS_PRE && !GRAD && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
             __syncthreads();
