@@ -484,14 +484,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_HEADS_K16 1
 #endif
 #ifndef FENV_PPO_SUMS_W2
-#define FENV_PPO_SUMS_W2 1
+#define FENV_PPO_SUMS_W2 0
 #endif
     constexpr bool kSW2 = kSpread && FENV_PPO_SUMS_W2;
 #ifndef FENV_PPO_LS_EARLY
 #define FENV_PPO_LS_EARLY 0
 #endif
 #ifndef FENV_PPO_LS_L2
-#define FENV_PPO_LS_L2 1
+#define FENV_PPO_LS_L2 0
 #endif
     constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
 #ifndef FENV_PPO_HG_VEC

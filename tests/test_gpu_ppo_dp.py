@@ -275,7 +275,6 @@ def test_fused_update_vs_torch_at_reference_config(mods):
 
     a0, p0, s0, smp = run(False, False)
     pert = [run(False, u)[1:3] for u in ("plus", "minus", "alt")]
-    torch.set_num_threads(min(8, torch.get_num_threads()))
     pert.append(run_cpu(a0, smp))
     a1, p1, s1, _ = run(True, False)
     assert torch.equal(a0, a1)
