@@ -9,4 +9,4 @@ for v in nprof1 nprof2; do
   echo "== PPO phase profile $v"
   FENV_LIB_OVERRIDE=$PWD/build_variants/libfenv_$v.so timeout -k 10 100 python -u tools/ppo_phase_profile.py 2>&1 | grep -v amdgpu.ids || exit $?
 done
-PAIRS=${PAIRS:-2} VARIANTS="${PPO_VARIANTS:-old pin1 ll0 sw0 lw0}" timeout -k 10 700 bash tools/ppo_variant_ab.sh 2>&1 | grep -v amdgpu.ids | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//; s/'samples_per_s'.*//"
+PAIRS=${PAIRS:-2} VARIANTS="${PPO_VARIANTS:-old pk0 tp0 pt0}" timeout -k 10 700 bash tools/ppo_variant_ab.sh 2>&1 | grep -v amdgpu.ids | sed -E "s/'note': [^}]*//; s/'workload': [^,]*,//; s/'samples_per_s'.*//"
