@@ -456,6 +456,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_SEP 1
 #endif
     constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
+#ifndef FENV_PPO_LOSS_DIV
+#define FENV_PPO_LOSS_DIV 0
+#endif
 #ifndef FENV_PPO_LOSS_SPREAD
 #define FENV_PPO_LOSS_SPREAD 1
 #endif
@@ -805,9 +808,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #else
                 if (!kLE && !kLL2 && (!kSpread || do_pi)) loss_consts();
                 const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
-                const float iv0 = lc_iv0, iv1 = lc_iv1;
-                (void)lc_var0;
-                (void)lc_var1;
+                const float iv0 = lc_iv0, iv1 = lc_iv1, var0 = lc_var0, var1 = lc_var1;
+                (void)var0;
+                (void)var1;
 #endif
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
@@ -820,8 +823,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                             const float mu0 = S[sMU0 * kPB + lane], mu1 = S[sMU1 * kPB + lane];
                             const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
                             const float d0 = a0 - mu0, d1 = a1 - mu1;
+#if FENV_PPO_LOSS_DIV  // torch's divisions (correctly rounded), not reciprocal products
+                            const float lp = (-(d0 * d0) / (2.0f * var0) - lsd0 - kLogSqrt2Pi) +
+                                             (-(d1 * d1) / (2.0f * var1) - lsd1 - kLogSqrt2Pi);
+#else
                             const float lp = (-(d0 * d0) * i2v0 - lsd0 - kLogSqrt2Pi) +
                                              (-(d1 * d1) * i2v1 - lsd1 - kLogSqrt2Pi);
+#endif
                             const float ratio = expf(lp - S[sOLP * kPB + lane]);
                             const float an = S[sADV * kPB + lane];
                             const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
@@ -834,10 +842,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                             const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
                             const float dratio = -(g1 * an + g2 * an * inside) * invB;
                             const float dlp = dratio * ratio;
+#if FENV_PPO_LOSS_DIV
+                            gmu0 = dlp * (d0 / var0);
+                            gmu1 = dlp * (d1 / var1);
+                            gls0 = dlp * ((d0 * d0) / var0 - 1.0f);
+                            gls1 = dlp * ((d1 * d1) / var1 - 1.0f);
+#else
                             gmu0 = dlp * (d0 * iv0);
                             gmu1 = dlp * (d1 * iv1);
                             gls0 = dlp * ((d0 * d0) * iv0 - 1.0f);
                             gls1 = dlp * ((d1 * d1) * iv1 - 1.0f);
+#endif
                         }
                         S[sGMU0 * kPB + lane] = gmu0;
                         S[sGMU1 * kPB + lane] = gmu1;
