@@ -138,6 +138,13 @@ __device__ __forceinline__ float tanh_u(float x) {
 #ifndef FENV_PPO_TANH_PK
 #define FENV_PPO_TANH_PK 1
 #endif
+// FENV_PPO_TANH_ACC: below |x| = 0.55 the exp form cancels (1 - 2/(1 + e^2x) loses up to
+// 1.4e-3 relative near 0, 1.6e-7 absolute); there an odd polynomial x + x^3 p(x^2) (degree-4 p,
+// a relative-error least-squares fit: <= 0.75 ulp over |x| < 0.55) is used instead, branch-free.
+// Above 0.55 the exp form is within ~3 ulp.  tools/tanh_fit.py derives the coefficients.
+#ifndef FENV_PPO_TANH_ACC
+#define FENV_PPO_TANH_ACC 1
+#endif
 __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
 #if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK
     using f2 = float __attribute__((ext_vector_type(2)));
@@ -146,7 +153,18 @@ __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1
     const f2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
     const f2 d = 1.0f + e;
     const f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    const f2 y = 1.0f - 2.0f * r;
+    f2 y = 1.0f - 2.0f * r;
+#if FENV_PPO_TANH_ACC
+    const f2 u = x * x;
+    f2 p = (f2)-0.006264324299991131f;
+    p = __builtin_elementwise_fma(p, u, (f2)0.02106410823762417f);
+    p = __builtin_elementwise_fma(p, u, (f2)-0.053850289434194565f);
+    p = __builtin_elementwise_fma(p, u, (f2)0.13332565128803253f);
+    p = __builtin_elementwise_fma(p, u, (f2)-0.33333316445350647f);
+    const f2 ys = __builtin_elementwise_fma(x * u, p, x);
+    y.x = __builtin_fabsf(x0) < 0.55f ? ys.x : y.x;
+    y.y = __builtin_fabsf(x1) < 0.55f ? ys.y : y.y;
+#endif
     y0 = y.x;
     y1 = y.y;
 #else
