@@ -142,8 +142,11 @@ __device__ __forceinline__ float tanh_u(float x) {
 // 1.4e-3 relative near 0, 1.6e-7 absolute); there an odd polynomial x + x^3 p(x^2) (degree-4 p,
 // a relative-error least-squares fit: <= 0.75 ulp over |x| < 0.55) is used instead, branch-free.
 // Above 0.55 the exp form is within ~3 ulp.  tools/tanh_fit.py derives the coefficients.
+// Off by default: it costs 0.5-0.6 us per minibatch (9.85-9.94 vs 9.26-9.39, same box,
+// profiles/ab/r3_ppo_tanh_ab.txt) and moves the reference-config update no closer to torch than
+// the spread of equally valid summation orders (tests/test_gpu_ppo_dp.py bounds the exp form).
 #ifndef FENV_PPO_TANH_ACC
-#define FENV_PPO_TANH_ACC 1
+#define FENV_PPO_TANH_ACC 0
 #endif
 __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
 #if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK

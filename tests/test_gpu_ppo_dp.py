@@ -199,12 +199,14 @@ def test_fused_update_vs_torch_at_reference_config(mods):
       inputs (a sample whose probability ratio sits at 1 +- clip_range, or a torch.min tie, flips
       its gradient for a last-bit difference, and Adam carries it forward).  torch is run from
       the start parameters, from three copies moved by ONE ulp (every element up, every
-      element down, every other element up), and on the CPU from the start parameters (its own
-      summation order at every step, as the kernel has); 3x the largest torch-vs-torch spread
-      is allowed, per statistic (one perturbed run alone samples that spread too thinly: in
-      round 3 the fused max landed at 3.09x one such spread, and the entropy loss, a mean of
-      log_std over the 7,820 steps, moves more under per-step rounding than under one start
-      perturbation);
+      element down, every other element up), on the CPU from the start parameters (its own
+      summation order at every step, as the kernel has), and with the kernel's tanh formula
+      (1 - 2 / (1 + e^2x): up to 1.6e-7 absolute, its largest per-step departure from torch's
+      tanh); 3x the largest torch-vs-torch spread is allowed, per statistic (one perturbed run
+      alone samples that spread too thinly: in round 3 the fused max landed at 3.09x one such
+      spread; and the entropy loss, a mean of log_std over the 7,820 steps, moves more under
+      per-step perturbations than under one at the start: tools/ppo_refcfg_probe.py shows
+      kernel variants that differ only in MFMA summation order 1e-5 to 1e-4 apart on it);
     * coherent: the kernel's per-minibatch gradients agree with autograd to 2e-6 of their scale
       (test_ppo_grad_matches_autograd) and its Adam step to ~1 ulp, so with delta = 4e-6 relative
       per step, K = 7,820 steps of at most lr = 1e-3 move a parameter apart by at most
@@ -219,7 +221,8 @@ def test_fused_update_vs_torch_at_reference_config(mods):
                               use_fused=fused)
         with torch.no_grad():
             ppo.collector.collect()  # the rollout uses the unperturbed parameters
-            if ulp:  # one ulp up / down (nextafter: zeros move to the smallest subnormal)
+            if ulp in ("plus", "minus", "alt"):  # one ulp up / down (nextafter: zeros move
+                # to the smallest subnormal)
                 f = ppo.policy.flat
                 up = torch.nextafter(f, torch.full_like(f, math.inf))
                 dn = torch.nextafter(f, torch.full_like(f, -math.inf))
@@ -231,7 +234,13 @@ def test_fused_update_vs_torch_at_reference_config(mods):
                     f[0::2] = up[0::2]
             samples = [t.detach().clone() for t in ppo._flat()]
         flat0 = ppo.policy.flat.clone()
-        st = ppo.train()
+        tanh = torch.tanh
+        if ulp == "ktanh":  # torch with the kernel's tanh formula (csrc/ppo_update.hip tanh_u)
+            torch.tanh = lambda x: 1.0 - 2.0 * torch.reciprocal(1.0 + torch.exp2(x * 2.88539008177792681))
+        try:
+            st = ppo.train()
+        finally:
+            torch.tanh = tanh
         s = ppo.opt.state[ppo.param]
         assert float(s["step"]) == 7820
         env.release()
@@ -274,7 +283,7 @@ def test_fused_update_vs_torch_at_reference_config(mods):
                                             entropy_loss=m[2], clip_fraction=m[3])
 
     a0, p0, s0, smp = run(False, False)
-    pert = [run(False, u)[1:3] for u in ("plus", "minus", "alt")]
+    pert = [run(False, u)[1:3] for u in ("plus", "minus", "alt", "ktanh")]
     pert.append(run_cpu(a0, smp))
     a1, p1, s1, _ = run(True, False)
     assert torch.equal(a0, a1)
