@@ -284,12 +284,38 @@ def test_metrics_and_partials(venv, F, N):
     obs, rew, done = env.rollout(torch.from_numpy(acts).to(DEV), partial=partial)
     rs, ds = 0.0, 0.0
     r = rew.cpu().numpy()
+    o = obs.cpu().numpy()
+    st_after = [v.cpu().numpy() for v in env.get_state()]
+    diag = []  # every mismatch, so that a failure records where it starts
     for k in range(8):
-        _, rr, rd, _ = ref.step(acts[k])
+        ro, rr, rd, _ = ref.step(acts[k])
         rs += rr.astype(np.float64).sum()
         ds += rd.sum()
-        # rewards first, bit for bit: a record mismatch below is then the records' own
-        assert np.array_equal(r[k].view(np.uint32), rr.view(np.uint32)), f"rewards, step {k}"
+        for what, a, b in (("obs", o[k], ro), ("rew", r[k], rr)):
+            bad = np.nonzero((a.view(np.uint32) != b.view(np.uint32)).reshape(F * N, -1).any(1))[0]
+            if bad.size:
+                diag.append(f"step {k} {what}: {bad.size} agents wrong, first {bad[0]} last "
+                            f"{bad[-1]} (formations {bad[0] // N}..{bad[-1] // N})")
+    if diag:
+        sr = ref.get_state()
+        bad = np.nonzero(st_after[0].view(np.uint32) != sr[0].view(np.uint32))[0]
+        diag.append(f"final px: {bad.size} agents wrong" + (f", first {bad[0]}" if bad.size else ""))
+        # which MT19937 draw set the step-4 reset applied to the wrong agents (2 is right)
+        if N <= 64:
+            import ctypes
+            from importlib import import_module
+            L = import_module(venv.__name__.rsplit(".", 1)[0] + "._lib")
+            for sset in (1, 2, 3):
+                hp = np.zeros(F * N, np.float32)
+                hq = np.zeros(F * N, np.float32)
+                g1 = np.zeros(F, np.float32)
+                g2 = np.zeros(F, np.float32)
+                L.lib().fenv_host_reset_draws(21, sset, F, 0, F, N, *(x.ctypes.data_as(
+                    ctypes.c_void_p) for x in (hp, hq, g1, g2)))
+                nx = (hp / np.float32(400)).astype(np.float32)  # obs column 0 of a fresh reset
+                same = np.nonzero(o[4][:, 0].view(np.uint32) == nx.view(np.uint32))[0]
+                diag.append(f"step-4 obs x matches draw set {sset} for {same.size} agents")
+    assert not diag, "; ".join(diag)
     recs = partial.cpu().numpy().astype(np.float64)
     if N <= 64:  # one record per 4 formation-waves: each equals its agents' reward sum
         per = 4 * (64 // N) * N

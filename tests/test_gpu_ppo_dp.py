@@ -38,6 +38,18 @@ def _params(mods, D, seed=0):
     return pol.flat.clone()
 
 
+def _groups(D):
+    """Flat-parameter ranges of SB3's MlpPolicy tensors (csrc/policy_device.h PLayout)."""
+    h = 64
+    sizes = [("pi0", h * D + h), ("pi2", h * h + h), ("vf0", h * D + h), ("vf2", h * h + h),
+             ("actW", 2 * h), ("actb", 2), ("valW", h), ("valb", 1), ("log_std", 2)]
+    out, o = {}, 0
+    for name, n in sizes:
+        out[name] = (o, o + n)
+        o += n
+    return out
+
+
 def _hp(L, cfg, lr=1e-3):
     return L.PPOHParams(clip_range=cfg.clip_range, ent_coef=cfg.ent_coef, vf_coef=cfg.vf_coef,
                         max_grad_norm=cfg.max_grad_norm, lr=lr, beta1=0.9, beta2=0.999, eps=1e-5,
@@ -103,7 +115,8 @@ def test_ppo_grad_matches_autograd(mods, D):
     the kernel's exp/rcp tanh (< 3e-7 absolute) are the only differences."""
     L = mods["_lib"]
     cfg = mods["ppo"].PPOConfig(batch_size=64, update_mode="sharded")
-    smp = _samples(300, D, 3)
+    smp = list(_samples(300, D, 3))
+    smp[4] = smp[4] * 135.0  # returns at the reference config's scale (value loss ~1.8e4)
     flat = _params(mods, D, 1)
     rows = torch.randperm(300, generator=torch.Generator().manual_seed(4))[:24].to(DEV)
     for ent_once in (1, 0):
@@ -122,6 +135,13 @@ def test_ppo_grad_matches_autograd(mods, D):
         scale = want.abs().max().item()
         err = (grad - want).abs().max().item()
         assert err <= 2e-6 * scale, (ent_once, err, scale)
+        # per parameter group too: the value head's gradient (large returns) must not hide an
+        # error in a small group such as log_std
+        for name, (a, b) in _groups(D).items():
+            gs = want[a:b].abs().max().item()
+            ge = (grad[a:b] - want[a:b]).abs().max().item()
+            print(f"grad group {name:8s} D={D} ent_once={ent_once} max|g| {gs:.3e} err {ge:.3e}")
+            assert ge <= 1e-5 * gs + 1e-9, (name, ge, gs)
         torch.testing.assert_close(sums, want_sums, rtol=1e-5, atol=1e-7)
     # no rows on this rank: a zero gradient (+ the entropy term where it lives)
     grad = torch.full_like(flat, 7.0)
