@@ -323,7 +323,15 @@ def test_fused_update_vs_torch_at_reference_config(mods):
     assert d_fused.median().item() <= 3 * u_med + coherent
     for k in s0:
         su = max(abs(p[1][k] - s0[k]) for p in pert)
-        assert abs(s1[k] - s0[k]) <= 3 * su + 1e-5 * max(1.0, abs(s0[k])), (k, s0[k], s1[k], su)
+        # the entropy loss is the mean of log_std along the trajectory, and log_std's gradient is
+        # a cancelling sum over the minibatch (sum of dlp (d^2 / var - 1)) whose summation order
+        # the kernel does not share with torch; kernel builds that differ from each other ONLY in
+        # MFMA summation order land 1.4e-5 .. 1.1e-4 apart on it (profiles/ab/r3_ppo_tanh_ab.txt,
+        # tools/ppo_refcfg_probe.py), while the per-minibatch log_std gradient itself matches
+        # autograd per parameter group to 1e-5 (test_ppo_grad_matches_autograd).  So the
+        # entropy mean gets 5e-5 relative on top of the torch spread; the others 1e-5.
+        rel = 5e-5 if k == "entropy_loss" else 1e-5
+        assert abs(s1[k] - s0[k]) <= 3 * su + rel * max(1.0, abs(s0[k])), (k, s0[k], s1[k], su)
 
 
 def test_ppo_sharded_mode_trains(mods):
