@@ -518,6 +518,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_LS_L2 0
 #endif
     constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
+#ifndef FENV_PPO_BC_WAVE
+#define FENV_PPO_BC_WAVE 1
+#endif
+    constexpr bool kBCW = SPLIT && !GRAD && FENV_PPO_BC_WAVE && !FENV_PPO_ADAM_PRE;
+    constexpr int kBC = 60;  // R slots: this minibatch's Adam step size and 1 / sqrt(bc2)
 #ifndef FENV_PPO_HG_VEC
 #define FENV_PPO_HG_VEC 1
 #endif
@@ -962,6 +967,18 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     }
                 }
                 }  // !kSpread
+            } else if (kBCW && wl == 1) {
+                // kBCW: this minibatch's Adam bias corrections (they depend on the step count
+                // only), by a wave that would otherwise wait out the loss at the barrier; every
+                // thread reads them after the norm exchange instead of computing them there
+                const float sn = step + 1.0f;
+                const float bc1 = 1.0f - exp2f(sn * lb1);  // 1 - beta1^step
+                const float bc2 = 1.0f - exp2f(sn * lb2);
+                const float ss = hp.lr / bc1, ib = 1.0f / __builtin_sqrtf(bc2);
+                if (lane == 0) {
+                    R[kBC] = ss;
+                    R[kBC + 1] = ib;
+                }
             }
             __syncthreads();
             FENV_PPO_PHASE(3);
@@ -1415,7 +1432,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             coef = coef < 1.0f ? coef : 1.0f;
             // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
             a_coef = coef;
-            if constexpr (!kAP) {
+            if constexpr (kBCW) {
+                step += 1.0f;
+                a_ss = R[kBC];
+                a_ib = R[kBC + 1];
+            } else if constexpr (!kAP) {
                 step += 1.0f;
                 const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
                 const float bc2 = 1.0f - exp2f(step * lb2);
