@@ -518,6 +518,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_LS_L2 0
 #endif
     constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
+#ifndef FENV_PPO_COEF_FAST
+#define FENV_PPO_COEF_FAST 1
+#endif
+#ifndef FENV_PPO_LC_FAST
+#define FENV_PPO_LC_FAST 1
+#endif
 #ifndef FENV_PPO_BC_WAVE
 #define FENV_PPO_BC_WAVE 1
 #endif
@@ -711,6 +717,22 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
             auto loss_consts = [&]() {
                 const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
+#if FENV_PPO_LC_FAST
+                // the loss wave's chain starts from these: hardware exp / log / reciprocal
+                // (v_exp_f32, v_log_f32, v_rcp_f32: ~1 ulp) instead of libm expf / logf and
+                // correctly rounded divisions (~70 dependent instructions)
+                const float kL2e = 1.44269504088896341f, kLn2 = 0.693147180559945309f;
+                const float sd0 = __builtin_amdgcn_exp2f(ls0 * kL2e);
+                const float sd1 = __builtin_amdgcn_exp2f(ls1 * kL2e);
+                lc_var0 = sd0 * sd0;
+                lc_var1 = sd1 * sd1;
+                lc_lsd0 = __builtin_amdgcn_logf(sd0) * kLn2;  // torch: std.log()
+                lc_lsd1 = __builtin_amdgcn_logf(sd1) * kLn2;
+                lc_iv0 = __builtin_amdgcn_rcpf(lc_var0);
+                lc_iv1 = __builtin_amdgcn_rcpf(lc_var1);
+                lc_i2v0 = 0.5f * lc_iv0;
+                lc_i2v1 = 0.5f * lc_iv1;
+#else
                 const float sd0 = expf(ls0), sd1 = expf(ls1);
                 lc_var0 = sd0 * sd0;
                 lc_var1 = sd1 * sd1;
@@ -720,6 +742,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 lc_i2v1 = 1.0f / (2.0f * lc_var1);
                 lc_iv0 = 1.0f / lc_var0;
                 lc_iv1 = 1.0f / lc_var1;
+#endif
             };
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
@@ -1427,8 +1450,15 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 tot = R[32];
             }
             FENV_PPO_PHASE(9);
+            // FENV_PPO_COEF_FAST: v_sqrt_f32 and v_rcp_f32 (1 ulp each) instead of the correctly
+            // rounded square root and division (~25 dependent instructions after the exchange)
+#if FENV_PPO_COEF_FAST
+            const float norm = __builtin_amdgcn_sqrtf(tot);
+            float coef = hp.max_grad_norm * __builtin_amdgcn_rcpf(norm + 1e-6f);
+#else
             const float norm = __builtin_sqrtf(tot);
             float coef = hp.max_grad_norm / (norm + 1e-6f);
+#endif
             coef = coef < 1.0f ? coef : 1.0f;
             // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
             a_coef = coef;
