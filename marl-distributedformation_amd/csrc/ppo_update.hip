@@ -518,6 +518,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_LS_L2 0
 #endif
     constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
+#ifndef FENV_PPO_DZ1_PRE
+#define FENV_PPO_DZ1_PRE 1
+#endif
+#ifndef FENV_PPO_HW_EARLY
+#define FENV_PPO_HW_EARLY 1
+#endif
+    constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
+    constexpr bool kHWE = SPLIT && FENV_PPO_HW_EARLY;
 #ifndef FENV_PPO_COEF_FAST
 #define FENV_PPO_COEF_FAST 1
 #endif
@@ -744,6 +752,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 lc_iv1 = 1.0f / lc_var1;
 #endif
             };
+            float hwv[16];  // kHWE: the heads' weight operands, read during layer 2
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
             // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
@@ -753,6 +762,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *Ar = H1 + (net * kPB + 32 * mt + c) * kRow + 32 * h;
                 const float *Bc = W + lx(net ? L.vf2W : L.pi2W) + (32 * nt + c) * kRow + 32 * h;
                 const float bias = W[lx((net ? L.vf2b : L.pi2b) + 32 * nt + c)];
+                if constexpr (kHWE) {  // the heads' weight operands (independent of layer 2)
+                    const int hq = lane >> 4, hc = lane & 15;
+                    const int hw = net ? L.valW : L.actW + (hc & 1) * kHid;
+#pragma unroll
+                    for (int s4 = 0; s4 < 16; ++s4)
+                        hwv[s4] = W[lx(hw + (FENV_PPO_HEADS_K16 ? 16 * hq + s4 : 4 * s4 + hq))];
+                }
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
@@ -813,7 +829,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     for (int s4 = 0; s4 < 16; ++s4) {
                         const int kk = FENV_PPO_HEADS_K16 ? 16 * q + s4 : 4 * s4 + q;
                         av[s4] = a[kk - q];
-                        wv[s4] = W[lx(hw + kk)];
+                        wv[s4] = kHWE ? hwv[s4] : W[lx(hw + kk)];
                     }
                     f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};  // kAcc2: two chains (even / odd steps)
 #pragma unroll
@@ -1188,6 +1204,17 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 f32x16 gw, dz;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) gw[r] = dz[r] = 0.0f;
+                // kDZP: tanh' = 1 - h1^2 of this wave's dL/dz1 tile, read and formed before the
+                // MFMA chains (h1 is read-only in this phase), so the tail after them is a product
+                float omh[16];
+                if constexpr (kDZP) {
+                    const float *H1p = H1 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float hv = H1p[rho(r, h) * kRow];
+                        omh[r] = 1.0f - hv * hv;
+                    }
+                }
 #if FENV_PPO_RING
                 // operands of step i + RD loaded while steps i.. issue (RD-deep register ring)
                 constexpr int RD = SPLIT ? FENV_PPO_RING_SPLIT : FENV_PPO_RING;
@@ -1295,8 +1322,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 float b1p = 0.0f;  // kB1: this lane's part of the b1 gradient of its column
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float hv = H1r[rho(r, h) * kRow];
-                    const float z1 = dz[r] * (1.0f - hv * hv);
+                    const float hv = kDZP ? 0.0f : H1r[rho(r, h) * kRow];
+                    const float z1 = kDZP ? dz[r] * omh[r] : dz[r] * (1.0f - hv * hv);
                     Z1w[rho(r, h) * kRow] = z1;
                     if (kB1) b1p += z1;
                 }
