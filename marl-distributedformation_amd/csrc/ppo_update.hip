@@ -522,7 +522,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_PRE 1
 #endif
 #ifndef FENV_PPO_HW_EARLY
-#define FENV_PPO_HW_EARLY 1
+#define FENV_PPO_HW_EARLY 0
 #endif
     constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
     constexpr bool kHWE = SPLIT && FENV_PPO_HW_EARLY;
