@@ -281,10 +281,12 @@ def test_metrics_and_partials(venv, F, N):
     ref.reset()
     acts = np.stack([synth_actions(4, k, F * N, 1.0) for k in range(8)])
     partial = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
-    obs, rew, done = env.rollout(torch.from_numpy(acts).to(DEV), partial=partial)
+    a_dev = torch.from_numpy(acts).to(DEV)
+    obs, rew, done = env.rollout(a_dev, partial=partial)
     rs, ds = 0.0, 0.0
     r = rew.cpu().numpy()
     o = obs.cpu().numpy()
+    a_back = a_dev.cpu().numpy()
     st_after = [v.cpu().numpy() for v in env.get_state()]
     diag = []  # every mismatch, so that a failure records where it starts
     for k in range(8):
@@ -297,6 +299,8 @@ def test_metrics_and_partials(venv, F, N):
                 diag.append(f"step {k} {what}: {bad.size} agents wrong, first {bad[0]} last "
                             f"{bad[-1]} (formations {bad[0] // N}..{bad[-1] // N})")
     if diag:
+        if not np.array_equal(a_back.view(np.uint32), acts.view(np.uint32)):
+            diag.append("the device actions differ from the host actions")
         sr = ref.get_state()
         bad = np.nonzero(st_after[0].view(np.uint32) != sr[0].view(np.uint32))[0]
         diag.append(f"final px: {bad.size} agents wrong" + (f", first {bad[0]}" if bad.size else ""))
