@@ -526,6 +526,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
     constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
     constexpr bool kHWE = SPLIT && FENV_PPO_HW_EARLY;
+#ifndef FENV_PPO_L2ROWS
+#define FENV_PPO_L2ROWS 1
+#endif
+    constexpr bool kL2R = SPLIT && FENV_PPO_L2ROWS && !FENV_PPO_LS_L2 && !FENV_PPO_HW_EARLY &&
+                          !FENV_PPO_LS_EARLY;
 #ifndef FENV_PPO_COEF_FAST
 #define FENV_PPO_COEF_FAST 1
 #endif
@@ -753,6 +758,80 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
             };
             float hwv[16];  // kHWE: the heads' weight operands, read during layer 2
+            if constexpr (kL2R) {
+            // ---- layer 2 by rows (FENV_PPO_L2ROWS, split launch): wave wl = samples
+            // 16 wl .. +15 x all 64 hidden units, as four 16 x 16 tiles on v_mfma_f32_16x16x4f32
+            // (K-step s of lane group q <-> hidden input 16 q + s: conflict-free operand reads;
+            // the A operand is shared by the four tiles).  With whole rows in the wave, the heads
+            // mu = actW . h2 + actb / value = valW . h2 + valb are per-lane products over its 4
+            // columns and a 16-lane DPP row sum: no heads phase, no barrier, no H2 re-read.
+            {
+                const int net = w >> 2, bt = wl, q = lane >> 4, c = lane & 15;
+                const float *Ar = H1 + (net * kPB + 16 * bt + c) * kRow + 16 * q;
+                const float *Bw = W + lx(net ? L.vf2W : L.pi2W) + c * kRow + 16 * q;
+                f32x4 acc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float bias = W[lx((net ? L.vf2b : L.pi2b) + 16 * t + c)];
+                    acc[t] = f32x4{bias, bias, bias, bias};
+                }
+#pragma unroll
+                for (int s4 = 0; s4 < 16; ++s4) {
+                    const float av = Ar[s4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Bw[16 * t * kRow + s4],
+                                                                     acc[t], 0, 0, 0);
+                }
+                // tanh, H2 rows (kept for the backward), and the heads' per-lane partials
+                const int hw0 = net ? L.valW : L.actW;
+                float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
+                float *Hr = H2 + (net * kPB + 16 * bt + 4 * q) * kRow + c;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float wa = W[lx(hw0 + 16 * t + c)];
+                    const float wb = net ? 0.0f : W[lx(L.actW + kHid + 16 * t + c)];
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        float y0, y1;
+                        tanh_u2(acc[t][r], acc[t][r + 1], y0, y1);
+                        Hr[r * kRow + 16 * t] = y0;
+                        Hr[(r + 1) * kRow + 16 * t] = y1;
+                        p0[r] = __builtin_fmaf(wa, y0, p0[r]);
+                        p0[r + 1] = __builtin_fmaf(wa, y1, p0[r + 1]);
+                        p1[r] = __builtin_fmaf(wb, y0, p1[r]);
+                        p1[r + 1] = __builtin_fmaf(wb, y1, p1[r + 1]);
+                    }
+                }
+                // sum over the 16 lanes of each row (hidden 16 t + c): lane 15 of the row holds it
+                auto rsum16 = [](float v) {
+                    int x = __float_as_int(v);
+                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
+                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
+                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false)));
+                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false)));
+                    return __int_as_float(x);
+                };
+                float m0[4], m1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    m0[r] = rsum16(p0[r]);
+                    m1[r] = net ? 0.0f : rsum16(p1[r]);
+                }
+                if (c == 15) {
+                    const float hb0 = W[lx(net ? L.valb : L.actb)];
+                    float *s0 = S + (net ? sVAL : sMU0) * kPB + 16 * bt + 4 * q;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s0[r] = m0[r] + hb0;
+                    if (!net) {
+                        const float hb1 = W[lx(L.actb + 1)];
+                        float *s1 = S + sMU1 * kPB + 16 * bt + 4 * q;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s1[r] = m1[r] + hb1;
+                    }
+                }
+            }
+            } else {
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
             // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
@@ -857,6 +936,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     for (int r = 0; r < 4; ++r) so[r] = acc[r] + hb;
                 }
             }
+            }  // !kL2R
             __syncthreads();
             FENV_PPO_PHASE(2);
             // ---- heads, losses and per-sample gradients (wave 0, lane = sample; split: wave 0 of
