@@ -775,14 +775,21 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     const float bias = W[lx((net ? L.vf2b : L.pi2b) + 16 * t + c)];
                     acc[t] = f32x4{bias, bias, bias, bias};
                 }
+                // operands read up front (the scheduler otherwise sinks each step's reads to
+                // their MFMAs, exposing the LDS latency once per step)
+                float av[16], bv[4][16];
 #pragma unroll
                 for (int s4 = 0; s4 < 16; ++s4) {
-                    const float av = Ar[s4];
+                    av[s4] = Ar[s4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) bv[t][s4] = Bw[16 * t * kRow + s4];
+                }
+#pragma unroll
+                for (int s4 = 0; s4 < 16; ++s4)
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Bw[16 * t * kRow + s4],
-                                                                     acc[t], 0, 0, 0);
-                }
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[t][s4], acc[t],
+                                                                     0, 0, 0);
                 // tanh, H2 rows (kept for the backward), and the heads' per-lane partials
                 const int hw0 = net ? L.valW : L.actW;
                 float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
@@ -790,7 +797,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const float wa = W[lx(hw0 + 16 * t + c)];
-                    const float wb = net ? 0.0f : W[lx(L.actW + kHid + 16 * t + c)];
+                    // branch-free: the critic reads its own row twice and drops the second sum
+                    const float wb = W[lx(net ? hw0 + 16 * t + c : L.actW + kHid + 16 * t + c)];
 #pragma unroll
                     for (int r = 0; r < 4; r += 2) {
                         float y0, y1;
@@ -816,7 +824,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     m0[r] = rsum16(p0[r]);
-                    m1[r] = net ? 0.0f : rsum16(p1[r]);
+                    m1[r] = rsum16(p1[r]);
                 }
                 if (c == 15) {
                     const float hb0 = W[lx(net ? L.valb : L.actb)];
