@@ -527,7 +527,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
     constexpr bool kHWE = SPLIT && FENV_PPO_HW_EARLY;
 #ifndef FENV_PPO_L2ROWS
-#define FENV_PPO_L2ROWS 1
+#define FENV_PPO_L2ROWS 0  // measured neutral-to-slower (profiles/ab/r3_ppo_l2rows_ab.txt)
 #endif
     constexpr bool kL2R = SPLIT && FENV_PPO_L2ROWS && !FENV_PPO_LS_L2 && !FENV_PPO_HW_EARLY &&
                           !FENV_PPO_LS_EARLY;
