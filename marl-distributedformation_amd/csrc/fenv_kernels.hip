@@ -164,7 +164,9 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
 // k_rollout_wave_split) gives one formation group two waves that both carry the state (the
 // kinematics, done and auto-reset are recomputed bit-identically by each): kRoleState writes
 // reward / done / the stats sums / the terminal and final state, kRoleObs only the observations.
-constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2;
+// FENV_SPLIT3 splits the observation work once more, by step parity: kRoleObsE writes the
+// observations of the even steps, kRoleObsO those of the odd ones (both still carry the state).
+constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2, kRoleObsE = 3, kRoleObsO = 4;
 
 template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll, bool NT = false,
           bool OB = false>
@@ -177,6 +179,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
                                              uint8_t *__restrict__ done, float &rsum,
                                              float &dsum, const RSStage &rsg = RSStage{}) {
     const int64_t A = c.F * (int64_t)c.N;
+    constexpr bool kObsR = ROLE == kRoleObs || ROLE == kRoleObsE || ROLE == kRoleObsO;
     Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
     if (active) {
         s.px = st.px[a];
@@ -217,7 +220,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
                                gen.k0, gen.k1);
             ac = (gs & 1) ? make_float2(act_u24(words.z), act_u24(words.w))
                           : make_float2(act_u24(words.x), act_u24(words.y));
-            if (ROLE != kRoleObs && gen.out && active)
+            if (!kObsR && gen.out && active)
                 reinterpret_cast<float2 *>(gen.out)[(int64_t)k * A + a] = ac;
         } else if (active && k + kPF < T) {
             ring[j] = act[(int64_t)(k + kPF) * A + a];
@@ -227,17 +230,22 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
             xpf = xlat_touch<D>(rsg, A, T, act, obs, rew, done);
         float rw;
         bool dn, rs;
-        env_step<MODE, X, ROLE != kRoleObs>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        env_step<MODE, X, !kObsR>(c, p, x, f, a, i, ac, s, rw, dn, rs);
         any_reset |= rs;
         const int64_t row = (int64_t)k * A + a;
-        float o[8];
-        env_obs<D>(x, s, o);
+        // step-parity roles: with an even prefetch depth the parity of k is the ring slot's
+        const int par = (kPF % 2 == 0 ? j : k) & 1;
+        const bool own = ROLE == kRoleObsE ? par == 0 : (ROLE == kRoleObsO ? par == 1 : true);
         if constexpr (OB) {  // obs non-NULL and 16-B aligned (the launcher checks)
+            float o[8];
+            env_obs<D>(x, s, o);
             store_obs_rows_buf<NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-        } else if (ROLE != kRoleState && obs) {
+        } else if (ROLE != kRoleState && obs && own) {
+            float o[8];
+            env_obs<D>(x, s, o);
             store_obs_rows<D, NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
         }
-        if (ROLE != kRoleObs && active) {
+        if (!kObsR && active) {
             if (RS) {
                 const int kb = k % kRSTB;
                 rsg.rbuf[kb * kRSA + rsg.li] = rw;
@@ -280,7 +288,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         }
     }
     if (FENV_XPF && RS) asm volatile("" ::"v"(xpf));  // the prefetch has landed before exit
-    if (ROLE != kRoleObs && active) {
+    if (!kObsR && active) {
         st.px[a] = s.px;
         st.py[a] = s.py;
         if (i == 0) {
@@ -345,8 +353,10 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
 // formations, so each wave issues about half of a step's instructions and a SIMD holds two
 // waves whose latencies hide each other.  The stats record is the 4 kRoleState waves' sums in
 // k_rollout_wave's order: the same records.
-template <int D, int MODE, bool RA, int PF>
-__global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState st, DevPending p,
+// OS (FENV_SPLIT3): three waves per formation-wave, the observation role split by step parity
+// (waves 4-7 the even steps' observations, waves 8-11 the odd steps').
+template <int D, int MODE, bool RA, int PF, bool OS = false>
+__global__ __launch_bounds__(OS ? 768 : 512) void k_rollout_wave_split(Consts c, DevState st, DevPending p,
                                                             int32_t T,
                                                             const float2 *__restrict__ act,
                                                             ActGen gen, float *__restrict__ obs,
@@ -354,7 +364,7 @@ __global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState s
                                                             uint8_t *__restrict__ done,
                                                             float2 *__restrict__ partial,
                                                             bool accum) {
-    __shared__ __attribute__((aligned(16))) float stage[4][64 * 8];
+    __shared__ __attribute__((aligned(16))) float stage[OS ? 8 : 4][64 * 8];
     __shared__ float2 red[4];
     const int lane = threadIdx.x & 63;
     const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -376,9 +386,17 @@ __global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState s
         rollout_body<D, MODE, RA, false, PF, WaveX, kRoleState>(
             c, st, p, x, active, f, a, i, nullptr, lane, M, f_first * N, T, act, gen, nullptr,
             rew, done, rsum, dsum);
-    else
+    else if (!OS)
         rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObs>(
             c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N, T, act, gen, obs,
+            nullptr, nullptr, rsum, dsum);
+    else if (w8 < 8)
+        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObsE>(
+            c, st, p, x, active, f, a, i, stage[w8 - 4], lane, M, f_first * N, T, act, gen, obs,
+            nullptr, nullptr, rsum, dsum);
+    else
+        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObsO>(
+            c, st, p, x, active, f, a, i, stage[w8 - 4], lane, M, f_first * N, T, act, gen, obs,
             nullptr, nullptr, rsum, dsum);
     if (partial) {
         if (w8 < 4) {
@@ -796,6 +814,9 @@ static inline bool use_pf(const Consts &c, int32_t T) {
 #ifndef FENV_SPLIT
 #define FENV_SPLIT 1
 #endif
+#ifndef FENV_SPLIT3
+#define FENV_SPLIT3 1
+#endif
 static inline bool use_split(const Consts &c) {
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
     return FENV_SPLIT && wave_path(c.N) && waves < FENV_RS_MIN_WAVES;
@@ -855,7 +876,14 @@ static hipError_t rollout_dmn(const Consts &c, const DevState &s, const DevPendi
                                a2, g0, obs, rew, done, p2, accum);
     } else if (use_split(c)) {
         const unsigned blocks = (unsigned)group_count(c);
-        if (use_pf(c, T))
+        if (FENV_SPLIT3 && use_pf(c, T))
+            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, FENV_SMALL_PF, true>),
+                               dim3(blocks), dim3(768), 0, st, c, s, p, T, a2, g0, obs, rew, done,
+                               p2, accum);
+        else if (FENV_SPLIT3)
+            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, 1, true>), dim3(blocks),
+                               dim3(768), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
+        else if (use_pf(c, T))
             hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, FENV_SMALL_PF>), dim3(blocks),
                                dim3(512), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
         else
@@ -920,7 +948,9 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
     if (large_path(c.N)) return "k_rollout_large";
     if (use_rs(c, T)) return "k_rollout_wave_rs";
     if (use_split(c))
-        return use_pf(c, T) ? "k_rollout_wave_split (prefetch 4)" : "k_rollout_wave_split";
+        return use_pf(c, T) ? (FENV_SPLIT3 ? "k_rollout_wave_split (3 roles, prefetch 4)"
+                                           : "k_rollout_wave_split (prefetch 4)")
+                            : (FENV_SPLIT3 ? "k_rollout_wave_split (3 roles)" : "k_rollout_wave_split");
     if (wave_path(c.N)) return use_pf(c, T) ? "k_rollout_wave (prefetch 4)" : "k_rollout_wave";
     return "k_rollout_block";
 }
