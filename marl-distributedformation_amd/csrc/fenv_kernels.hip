@@ -815,7 +815,7 @@ static inline bool use_pf(const Consts &c, int32_t T) {
 #define FENV_SPLIT 1
 #endif
 #ifndef FENV_SPLIT3
-#define FENV_SPLIT3 1
+#define FENV_SPLIT3 0  // measured slower at config 1 (profiles/ab/r3_config1_split3_ab.txt)
 #endif
 static inline bool use_split(const Consts &c) {
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
