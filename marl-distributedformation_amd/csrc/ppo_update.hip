@@ -1112,7 +1112,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // kSpread: the loss sums, one or two per wave of waves 1-3 (wave 0 just ran the loss);
             // their outputs are only read from the norm phase on (kSW2: taken in the shadow of
             // the W2-gradient MFMAs instead, below)
-            if constexpr (kSpread && !kSW2) {
+            // FENV_PPO_SUMS_LATE: after this phase's head-gradient / dL/dz2 work instead of before
+            auto loss_sums = [&]() {
                 if (net_b == 0) {
                     if (wl == 1) {
                         const float spl = wsum(S[sPL * kPB + lane]), scf = wsum(S[sCF * kPB + lane]);
@@ -1152,7 +1153,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         }
                     }
                 }
-            }
+            };
+#ifndef FENV_PPO_SUMS_LATE
+#define FENV_PPO_SUMS_LATE 1
+#endif
+            if constexpr (kSpread && !kSW2 && !FENV_PPO_SUMS_LATE) loss_sums();
             // ---- head weight gradients on v_mfma_f32_16x16x4f32 (wave w = net w>>2, hidden rows
             // 16(w&3)..+15, columns gmu0/gmu1 resp. gv; K = 64 samples as 16 MFMAs), then
             // dL/dz2 in place over the SAME H2 columns (only this wave reads or writes them in
@@ -1239,6 +1244,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         gss = __builtin_fmaf(acc[r], acc[r], gss);
                     }
                 }
+                if constexpr (kSpread && !kSW2 && FENV_PPO_SUMS_LATE) loss_sums();
             } else {
                 const int net = w >> 2, kt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
