@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 }
             };
 #ifndef FENV_PPO_SUMS_LATE
-#define FENV_PPO_SUMS_LATE 1
+#define FENV_PPO_SUMS_LATE 0  // measured neutral (profiles/ab/r3_ppo_sums_late_ab.txt)
 #endif
             if constexpr (kSpread && !kSW2 && !FENV_PPO_SUMS_LATE) loss_sums();
             // ---- head weight gradients on v_mfma_f32_16x16x4f32 (wave w = net w>>2, hidden rows
