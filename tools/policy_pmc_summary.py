@@ -12,18 +12,21 @@ import os
 import sys
 
 src, out = sys.argv[1], sys.argv[2]
+kpat = sys.argv[3] if len(sys.argv) > 3 else "k_policy"  # kernel-name filter
+prefix = sys.argv[4] if len(sys.argv) > 4 else "ppmc_"   # output directories of the passes
+what = sys.argv[5] if len(sys.argv) > 5 else ("tools/policy_pmc.sh) over tools/rollout_timing.py, "
+                                               "config 2 (65536 x 10)")
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(os.path.join(src, "ppmc_*", "**", "*counter_collection*.csv"), recursive=True):
+for f in glob.glob(os.path.join(src, prefix + "*", "**", "*counter_collection*.csv"), recursive=True):
     per = collections.defaultdict(float)  # (kernel, dispatch, counter) -> value (sum over dims)
     for row in csv.DictReader(open(f)):
         k = row.get("Kernel_Name", "")
-        if "k_policy" not in k:
+        if kpat not in k:
             continue
         per[(k.split("(")[0], row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
     for (k, _, c), v in per.items():
         acc[k][c].append(v)
-res = {"source": "rocprofv3 --pmc passes (tools/policy_pmc.sh) over tools/rollout_timing.py, "
-                 "config 2 (65536 x 10), per dispatch averages",
+res = {"source": "rocprofv3 --pmc passes (" + what + ", per dispatch averages",
        "units": "SQ_* cycle counters in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES; summed over "
                 "the chip",
        "kernels": {k: {c: sum(v) / len(v) for c, v in sorted(cs.items())}
