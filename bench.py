@@ -3,11 +3,11 @@
 
 Metric (BASELINE.json): agent-steps/sec (whole node) at 5 agents/formation, and the step
 kernel's fraction of the HBM roofline.  Workload: BASELINE config 3 -- 1,048,576 formations x 5
-agents (5,242,880 agents) per GPU.  Formations are independent, so the ranks own disjoint
-contiguous formation shards of one global env with no data-path collective (weak scaling: N
-GPUs step N x 1M formations; `--strong` instead splits `--formations` over the ranks, i.e. config
-3's literal 1M formations over 8 GPUs, and tools/shard_sizes.sh measures those shard sizes on
-one GPU).  A "step" is one env step of every agent; steps run as fused rollouts of
+agents (5,242,880 agents).  Formations are independent, so the ranks own disjoint contiguous
+formation shards of one global env with no data-path collective.  With N > 1 GPUs the headline
+is config 3 as written -- the 1M formations split over the ranks (strong scaling, `"scaling":
+"strong"`) -- and the same line nests the weak-scaling measurement (1M formations on every rank,
+`weak_scaling_line`); `--scaling weak` swaps the two, `--no-weak-line` skips the nested one.  A "step" is one env step of every agent; steps run as fused rollouts of
 `--chunk` steps per launch (SB3's n_steps=10 rollout, vectorized_env.py:128) writing obs /
 reward / done for every step into a device rollout buffer, with the actions read from HBM
 (inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
@@ -452,54 +452,17 @@ def stagger_episodes(env, pdist_first: int) -> None:
     env.set_state(px, py, gx, gy, t)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--formations", type=int, default=1 << 20,
-                    help="formations per GPU (weak scaling), or in total with --strong")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: shard --formations over the ranks")
-    ap.add_argument("--agents", type=int, default=5)
-    ap.add_argument("--chunk", type=int, default=10)
-    ap.add_argument("--reset-mode", default="philox", choices=["philox", "mt19937"])
-    ap.add_argument("--episode-phase", default="staggered", choices=["staggered", "aligned"],
-                    help="staggered (philox only): formations spread over the episode, so every "
-                         "window includes resets; aligned: all start at t=0 like the reference")
-    ap.add_argument("--no-goal", action="store_true")
-    ap.add_argument("--prewarm-ms", type=float, default=400.0,
-                    help="device-time pre-warm (clocks, first-touch of the buffers) before the "
-                         "--warmup steps; independent of --warmup, reported as warmup_ms")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-stats", action="store_true")
-    ap.add_argument("--stats-every", type=int, default=10,
-                    help="reduce + all-reduce the episode stats every this many rollout launches "
-                         "(clamped to the timed launch count)")
-    ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
-    ap.add_argument("--no-configs", action="store_true",
-                    help="skip the secondary env-only lines (BASELINE configs[1] and [4])")
-    args = ap.parse_args()
-    if args.steps < 1 or args.warmup < 0 or args.chunk < 1:
-        ap.error("need --steps >= 1, --warmup >= 0, --chunk >= 1")
-
+def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, scaling: str):
+    """One headline measurement (BASELINE config 3 shape) over `total_formations` formations
+    sharded contiguously over the ranks; returns the JSON line's fields on rank 0, None
+    elsewhere.  Every rank builds its own shard env, buffers and streams; the env is released
+    before returning so a second measurement starts from free HBM."""
     import torch
-    import pkgload
-    pkg = pkgload.load()
     from importlib import import_module
     venv = import_module(pkg.__name__ + ".vectorized_env")
     pdist = import_module(pkg.__name__ + ".distributed")
-
-    rank, world, local = pdist.init_from_env()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-
     N, T = args.agents, args.chunk
     D = 6 if args.no_goal else 8
-    total_formations = args.formations if args.strong else args.formations * world
     first, F = pdist.shard_range(total_formations, rank, world)
     cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": not args.no_goal}
     env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode=args.reset_mode,
@@ -653,7 +616,8 @@ def main():
     bytes_timed = sum(rollout_bytes_per_launch(A, N, D, L) for L in plan)
     achieved = bytes_timed / (kern_total_ms * 1e-3) / 1e9
     workload = (f"config3: {total_formations} formations x {N} agents "
-                f"({F} per GPU x {world}), fused {T}-step rollouts, {args.reset_mode} resets")
+                f"({F} per GPU x {world}), fused {T}-step rollouts, {args.reset_mode} resets"
+                + ("" if world == 1 else f", {scaling} scaling"))
     traffic, tsrc = load_pmc_traffic(workload if world == 1 else "")
     kname = env.rollout_kernel_name(T)
     if rank == 0:
@@ -666,7 +630,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: U(-1,1) fp32 actions resident in HBM, random-init formations",
@@ -677,7 +641,10 @@ def main():
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
                        "episode_phase": phase, "timed_launches": plan,
-                       "parallelism": f"formation-shard dp{world}"},
+                       "parallelism": f"formation-shard dp{world} ({scaling}: "
+                                       + ("formations split over the ranks"
+                                          if scaling == "strong" else
+                                          f"{F} formations per rank") + ")"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": tsrc,
@@ -711,6 +678,84 @@ def main():
             out["episode_stats"] = {"mean_reward_sampled_rollout": t[0] / (total_agents * sampled),
                                     "agent_dones_sampled_rollout": t[1],
                                     "every_launches": stat_every}
+        return out, env
+    return None, env
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--formations", type=int, default=1 << 20,
+                    help="formations in total (strong scaling, the N > 1 default), or per GPU "
+                         "(weak scaling)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: shard --formations over the ranks (= --scaling strong)")
+    ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
+                    help="auto: strong for N > 1 (BASELINE config 3: 1M formations sharded over "
+                         "the GPUs), weak (= strong) at N = 1")
+    ap.add_argument("--no-weak-line", action="store_true",
+                    help="N > 1: skip the second (other-scaling) measurement nested in the line")
+    ap.add_argument("--agents", type=int, default=5)
+    ap.add_argument("--chunk", type=int, default=10)
+    ap.add_argument("--reset-mode", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--episode-phase", default="staggered", choices=["staggered", "aligned"],
+                    help="staggered (philox only): formations spread over the episode, so every "
+                         "window includes resets; aligned: all start at t=0 like the reference")
+    ap.add_argument("--no-goal", action="store_true")
+    ap.add_argument("--prewarm-ms", type=float, default=400.0,
+                    help="device-time pre-warm (clocks, first-touch of the buffers) before the "
+                         "--warmup steps; independent of --warmup, reported as warmup_ms")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--stats-every", type=int, default=10,
+                    help="reduce + all-reduce the episode stats every this many rollout launches "
+                         "(clamped to the timed launch count)")
+    ap.add_argument("--no-policy", action="store_true", help="skip the config-2 policy rollout")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the secondary env-only lines (BASELINE configs[1] and [4])")
+    args = ap.parse_args()
+    if args.steps < 1 or args.warmup < 0 or args.chunk < 1:
+        ap.error("need --steps >= 1, --warmup >= 0, --chunk >= 1")
+
+    import torch
+    import pkgload
+    pkg = pkgload.load()
+    from importlib import import_module
+    pdist = import_module(pkg.__name__ + ".distributed")
+
+    rank, world, local = pdist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    N = args.agents
+    D = 6 if args.no_goal else 8
+    if args.scaling == "auto":
+        scaling = "strong" if world > 1 else "weak"
+    else:
+        scaling = args.scaling
+    if args.strong:
+        scaling = "strong"
+    # BASELINE config 3 as written: 1,048,576 formations sharded over the GPUs (strong); the
+    # weak line (1,048,576 formations on every GPU) rides along as a nested measurement
+    total = args.formations if scaling == "strong" else args.formations * world
+    out, env = run_config3(args, pkg, rank, world, dev, total, scaling)
+    env.release()
+    del env
+    if world > 1 and not args.no_weak_line:
+        other = "weak" if scaling == "strong" else "strong"
+        tot2 = args.formations * world if other == "weak" else args.formations
+        o2, env2 = run_config3(args, pkg, rank, world, dev, tot2, other)
+        env2.release()
+        del env2
+        if rank == 0:
+            keep = ("value", "ms_per_step", "scaling", "config", "roofline", "steps")
+            out[f"{other}_scaling_line"] = {k: o2[k] for k in keep}
+    if rank == 0:
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = secondary(policy_rollout_bench, pkg.__name__, dev, 65536, 10,
                                               10)

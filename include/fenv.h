@@ -34,8 +34,9 @@ extern "C" {
  * gets a new symbol name, never a reordered argument list under the old one.
  *   1  round-1/2 entry points (policy_forward with row0)
  *   2  + fenv_abi_version, fenv_get_state_range, fenv_metrics_range, ppo_workspace_bytes,
- *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject */
-#define FENV_ABI_VERSION 2
+ *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject
+ *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes (no signature changed) */
+#define FENV_ABI_VERSION 3
 int fenv_abi_version(void);
 
 typedef struct fenv fenv_t;
@@ -74,9 +75,30 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
 /* Frees the handle and every device/pinned buffer it owns.  Safe at any point: it restores the
  * caller's current device, waits for the handle's own staging copy (hipFree then waits for the
  * device's work), and a free that the runtime refuses because a stream capture is under way is
- * parked and retried by the next fenv_create / fenv_destroy.  A second destroy of the same
- * handle is detected where the memory still holds it and returns FENV_EINVAL. */
+ * parked and retried by the next fenv_create / fenv_destroy.  The library keeps the set of live
+ * handles: a pointer not in it (a second destroy, or never created) returns FENV_EINVAL without
+ * its memory being read. */
 int fenv_destroy(fenv_t *env);
+
+/* FENV_RESET_MT19937 staging check.  Every staged reset set carries per-draw tags (computed from
+ * the draws' bits, their index and the set's generation); the kernels verify them when they apply
+ * a reset, and a failure is recorded in the handle.  From then on every call on the handle
+ * (fenv_reset, fenv_observe, fenv_step, fenv_rollout*, fenv_policy_rollout, fenv_metrics*,
+ * fenv_get_state*, fenv_set_state, fenv_status) returns FENV_ESTATE with a message naming the
+ * generation, the formation and whether the set read was the slot's previous one, the other
+ * slot's, or neither.  A failure is seen by the first call after the failing launch has run:
+ * fenv_status after a synchronize of the launch stream reports it (host read, no GPU call). */
+int fenv_status(const fenv_t *env);
+
+/* Test hooks of the MT19937 staging (host only).  The next n_refills staging copies, of any
+ * handle, run in `mode`: 1 = the copy kernel sleeps ~0.35 ms first (a launch that were not
+ * ordered behind its refill would read the slot's old set); 2 = the copy is skipped (the slot
+ * keeps its old set: the tag check must fire).  mode 0 / n_refills 0 turns the hook off. */
+void fenv_test_stage_hook(int32_t mode, int32_t n_refills);
+
+/* Bytes of pinned staging buffers cached for reuse on `device` (bounded at 512 MiB per device;
+ * a destroyed env's buffer is freed instead when the pool is full). */
+int64_t fenv_pinned_pool_bytes(int32_t device);
 
 /* out_host[0..7] = {num_formation, num_agents, obs_dim, num_agents_total(A), steps_since_reset
  * (common value, -1 if formations differ), reset_mode, first_formation, total_formations}. */

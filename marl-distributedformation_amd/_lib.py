@@ -67,6 +67,9 @@ SIGNATURES = {
                         ctypes.c_float, _I32, _I32, _P, _P, _P, _P]),
     "ppo_apply": (_I32, [_P, _P, _P, _P, _P, _I32, _P, _P]),
     "fenv_test_ppo_inject": (None, [_I32]),
+    "fenv_status": (_I32, [_P]),
+    "fenv_test_stage_hook": (None, [_I32, _I32]),
+    "fenv_pinned_pool_bytes": (_I64, [_I32]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
 

@@ -66,6 +66,21 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 // torch.rand float32 from 32 random bits: (r & 0xFFFFFF) * 2^-24 (exact).
 __device__ __forceinline__ float u24(uint32_t r) { return (float)(r & 0xFFFFFFu) * 0x1.0p-24f; }
 
+// A staged MT19937 draw failed its tag check (fenv_internal.h DevPending): classify it against the
+// generations the slot and the other slot held, and record it in the handle's error words (host
+// memory; relaxed system-scope vector stores -- any lane's values will do).
+static __device__ __attribute__((noinline)) void stage_tag_fail(const DevPending &p, int64_t f, int64_t a,
+                                                         uint32_t tag, uint32_t bx, uint32_t by) {
+    uint32_t kind = kStageBad;
+    if (tag == stage_tag_agent(p.gen - 2u, a, bx, by)) kind = kStageStale;
+    else if (tag == stage_tag_agent(p.gen - 1u, a, bx, by) ||
+             tag == stage_tag_agent(p.gen + 1u, a, bx, by)) kind = kStageOther;
+    if (p.err == nullptr) return;
+    __hip_atomic_store(p.err + 0, kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.err + 1, p.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.err + 2, (uint32_t)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // simulate.py:133-143 for agent i of formation f (local indices), episode `ep_new`.
 template <int MODE>
 __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p, int64_t f,
@@ -77,6 +92,13 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
         py = p.pend[A + a];
         gx = p.pend[2 * A + f];
         gy = p.pend[2 * A + c.F + f];
+        const uint32_t *tg = reinterpret_cast<const uint32_t *>(p.pend + 2 * A + 2 * c.F);
+        const uint32_t ta = tg[a], tf = tg[A + f];
+        const uint32_t bx = __float_as_uint(px), by = __float_as_uint(py);
+        if (ta != stage_tag_agent(p.gen, a, bx, by))
+            stage_tag_fail(p, f, a, ta, bx, by);
+        else if (tf != stage_tag_goal(p.gen, f, __float_as_uint(gx), __float_as_uint(gy)))
+            stage_tag_fail(p, f, a, 0u, 0u, 0u);  // the goal's tag: kStageBad
     } else {
         const uint64_t fg = (uint64_t)(c.f0 + f);
         const uint64_t ag = fg * (uint64_t)c.N + (uint64_t)i;

@@ -8,10 +8,12 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <random>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "fenv.h"
@@ -85,25 +87,32 @@ void free_host(int32_t device, void *p) {
         graveyard().host.emplace_back(device, p);
     }
 }
-// Pinned staging buffers of the MT19937 reset sets are pooled for the process and never freed:
-// a destroyed env's buffer goes back to the pool and the next env takes it (smallest that fits),
-// so host staging addresses are never released and re-mapped while the process runs.
+// Pinned staging buffers of the MT19937 reset sets are pooled per device: a destroyed env's
+// buffer goes back to its device's pool and the next env on that device takes the smallest that
+// fits (never one more than 4x the request), so host staging addresses are not released and
+// re-mapped on every env churn.  The pool is bounded: a buffer returned while the device's pool
+// already caches kPoolCap bytes is freed (hipHostFree, parked if a capture is under way).
+constexpr size_t kPoolCap = (size_t)512 << 20;
 struct PinnedPool {
     std::mutex mu;
-    std::multimap<size_t, std::pair<float *, float *>> free;  // bytes -> (host, device address)
+    // device -> (bytes -> (host, device address))
+    std::map<int32_t, std::multimap<size_t, std::pair<float *, float *>>> free;
+    std::map<int32_t, size_t> cached;
 };
 PinnedPool &pinned_pool() {
     static PinnedPool *p = new PinnedPool();  // never destroyed: usable from atexit / finalizers
     return *p;
 }
-hipError_t pinned_take(size_t bytes, float **host, float **dev) {
+hipError_t pinned_take(int32_t device, size_t bytes, float **host, float **dev) {
     {
         std::lock_guard<std::mutex> lk(pinned_pool().mu);
-        auto it = pinned_pool().free.lower_bound(bytes);
-        if (it != pinned_pool().free.end()) {
+        auto &fl = pinned_pool().free[device];
+        auto it = fl.lower_bound(bytes);
+        if (it != fl.end() && it->first <= 4 * bytes) {
             *host = it->second.first;
             *dev = it->second.second;
-            pinned_pool().free.erase(it);
+            pinned_pool().cached[device] -= it->first;
+            fl.erase(it);
             return hipSuccess;
         }
     }
@@ -123,12 +132,29 @@ hipError_t pinned_take(size_t bytes, float **host, float **dev) {
     *dev = reinterpret_cast<float *>(reinterpret_cast<char *>(d) + 256);
     return hipSuccess;
 }
-void pinned_give(float *host, float *dev) {
+void pinned_give(int32_t device, float *host, float *dev) {
     if (!host) return;
-    const size_t bytes = *reinterpret_cast<size_t *>(reinterpret_cast<char *>(host) - 256);
-    std::lock_guard<std::mutex> lk(pinned_pool().mu);
-    pinned_pool().free.emplace(bytes, std::make_pair(host, dev));
+    char *base = reinterpret_cast<char *>(host) - 256;
+    const size_t bytes = *reinterpret_cast<size_t *>(base);
+    {
+        std::lock_guard<std::mutex> lk(pinned_pool().mu);
+        size_t &c = pinned_pool().cached[device];
+        if (c + bytes <= kPoolCap) {
+            pinned_pool().free[device].emplace(bytes, std::make_pair(host, dev));
+            c += bytes;
+            return;
+        }
+    }
+    free_host(device, base);
 }
+size_t pinned_cached(int32_t device) {
+    std::lock_guard<std::mutex> lk(pinned_pool().mu);
+    auto it = pinned_pool().cached.find(device);
+    return it == pinned_pool().cached.end() ? 0 : it->second;
+}
+// Test hook of the staging (fenv_test_stage_hook): the next g_stage_n refills run in mode
+// g_stage_mode (1: the copy kernel sleeps first; 2: the copy is skipped).
+std::atomic<int32_t> g_stage_mode{0}, g_stage_n{0};
 // Retry the parked frees (each is parked again if a capture is still under way).
 void drain_graveyard() {
     std::vector<std::pair<int32_t, void *>> dev, host;
@@ -144,12 +170,28 @@ void drain_graveyard() {
     for (auto &h : host) free_host(h.first, h.second);
 }
 
-constexpr uint64_t kLive = 0x666e65762d6c6976ull;  // "fenv-liv": a handle not yet destroyed
+// Live handles: fenv_create registers, fenv_destroy takes out.  A pointer that is not in the set
+// (destroyed already, or never created) is refused without touching its memory.
+struct LiveSet {
+    std::mutex mu;
+    std::unordered_set<const void *> set;
+};
+LiveSet &live() {
+    static LiveSet *l = new LiveSet();  // never destroyed: usable from atexit / finalizers
+    return *l;
+}
+void live_add(const void *e) {
+    std::lock_guard<std::mutex> lk(live().mu);
+    live().set.insert(e);
+}
+bool live_take(const void *e) {
+    std::lock_guard<std::mutex> lk(live().mu);
+    return live().set.erase(e) == 1;
+}
 
 }  // namespace
 
 struct fenv {
-    uint64_t magic = kLive;
     int32_t device = 0;
     fenvk::Consts c{};
     int32_t D = 8;
@@ -166,6 +208,10 @@ struct fenv {
     float *pend = nullptr;
     float *hpend = nullptr;
     float *hpend_dev = nullptr;
+    uint32_t gen_next = 1;                // generation of the next set drawn (1: the ctor's)
+    uint32_t slot_gen[2] = {0u, 0u};      // generation each slot holds
+    uint32_t *err_host = nullptr;         // the kernels' staging error words [4] (pinned)
+    uint32_t *err_dev = nullptr;          // their mapped device address
     hipEvent_t pend_ev[2] = {nullptr, nullptr};  // staging copy of slot k done
     hipEvent_t used_ev[2] = {nullptr, nullptr};  // the launch that consumed slot k is done
     bool pend_ev_recorded[2] = {false, false};
@@ -178,11 +224,25 @@ struct fenv {
     std::mt19937 mt;         // the reference's global stream (all formations of all shards)
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
 
-    size_t pend_floats() const { return (size_t)(2 * A + 2 * c.F); }
+    size_t pend_floats() const { return (size_t)fenvk::stage_floats(A, c.F); }
     size_t pend_stride() const { return (pend_floats() + 63) & ~(size_t)63; }  // 256-B slots
     fenvk::DevPending pending() const {
         return fenvk::DevPending{pend ? pend + (size_t)rd * pend_stride() : nullptr,
-                                 reinterpret_cast<float4 *>(term), lf};
+                                 reinterpret_cast<float4 *>(term), lf, err_dev, slot_gen[rd]};
+    }
+
+    // A staged set failed the kernels' tag check in an earlier launch (DevPending): the state
+    // may hold wrong draws, so every later call on the handle fails.
+    int stage_check() const {
+        if (!err_host || err_host[0] == 0u) return FENV_OK;
+        static const char *kinds[] = {"", "the slot's previous set (two refills back)",
+                                      "the other slot's set", "neither set (corrupt)"};
+        const uint32_t k = err_host[0] < 4u ? err_host[0] : 3u;
+        return fail(FENV_ESTATE, std::string("MT19937 reset: a kernel read a staged draw set "
+                                             "that failed its tag check (generation ") +
+                                     std::to_string(err_host[1]) + ", formation " +
+                                     std::to_string(err_host[2]) + "): it read " + kinds[k] +
+                                     "; the env state is not the reference's -- recreate it");
     }
 
     // A launch that may read the staged set waits (on the device) for its refill, which may have
@@ -208,12 +268,30 @@ struct fenv {
         mt.discard(per * (uint64_t)c.f0);
         float *hp = hpend + off;
         float *px = hp, *py = hp + A, *gx = hp + 2 * A, *gy = hp + 2 * A + c.F;
-        for (int64_t f = 0; f < c.F; ++f)
+        uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F), *gt = at + A;
+        const uint32_t gen = gen_next++;
+        for (int64_t f = 0; f < c.F; ++f) {
             draw_formation(mt, c.N, px + f * c.N, py + f * c.N, gx[f], gy[f]);
+            for (int64_t a = f * c.N; a < (f + 1) * c.N; ++a) {
+                uint32_t bx, by;
+                std::memcpy(&bx, px + a, 4);
+                std::memcpy(&by, py + a, 4);
+                at[a] = fenvk::stage_tag_agent(gen, a, bx, by);
+            }
+            uint32_t bx, by;
+            std::memcpy(&bx, gx + f, 4);
+            std::memcpy(&by, gy + f, 4);
+            gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
+        }
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
         // the slot's previous reader (the launch that consumed it, on whatever stream) first
         if (used_ev_recorded[w]) FENV_HIP(hipStreamWaitEvent(st, used_ev[w], 0));
-        FENV_HIP(fenvk::launch_stage_copy(pend + off, hpend_dev + off, (int64_t)pend_floats(), st));
+        int32_t mode = 0;
+        if (g_stage_n.load() > 0 && g_stage_n.fetch_sub(1) > 0) mode = g_stage_mode.load();
+        if (mode != 2)
+            FENV_HIP(fenvk::launch_stage_copy(pend + off, hpend_dev + off,
+                                              (int64_t)pend_floats(), mode == 1 ? 100 : 0, st));
+        slot_gen[w] = gen;
         FENV_HIP(hipEventRecord(pend_ev[w], st));
         pend_ev_recorded[w] = true;
         rd = w;
@@ -275,6 +353,7 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     FENV_HIP(hipSetDevice(device));
 
     fenv *e = new fenv();
+    live_add(e);
     e->device = device;
     e->goal_in_obs = goal_in_obs ? 1 : 0;
     e->D = goal_in_obs ? 8 : 6;  // vectorized_env.py:28-31
@@ -326,8 +405,15 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
         const size_t pb = 2 * e->pend_stride() * sizeof(float);
         he = hipMalloc(&e->pend, pb);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipMalloc(pending) failed"));
-        he = pinned_take(pb + 256, &e->hpend, &e->hpend_dev);
+        he = pinned_take(device, pb + 256, &e->hpend, &e->hpend_dev);
         if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipHostMalloc(pending) failed"));
+        he = hipHostMalloc(reinterpret_cast<void **>(&e->err_host), 64,
+                           hipHostMallocMapped | hipHostMallocCoherent);
+        if (he == hipSuccess) {
+            std::memset(e->err_host, 0, 64);
+            he = hipHostGetDevicePointer(reinterpret_cast<void **>(&e->err_dev), e->err_host, 0);
+        }
+        if (he != hipSuccess) return cleanup(fail(FENV_ENOMEM, "hipHostMalloc(error words) failed"));
         for (int k = 0; k < 2; ++k) {
             he = hipEventCreateWithFlags(&e->pend_ev[k], hipEventDisableTiming);
             if (he == hipSuccess) he = hipEventCreateWithFlags(&e->used_ev[k], hipEventDisableTiming);
@@ -348,8 +434,7 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
 
 int fenv_destroy(fenv_t *e) {
     if (!e) return FENV_OK;
-    if (e->magic != kLive) return fail(FENV_EINVAL, "fenv_destroy: not a live handle (destroyed twice?)");
-    e->magic = 0;
+    if (!live_take(e)) return fail(FENV_EINVAL, "fenv_destroy: not a live handle (destroyed twice?)");
     // Safe at any point: the caller's current device is restored; the handle's own staging copy
     // is waited for (hipFree then waits for the device's kernels); a free the runtime refuses
     // during a stream capture is parked and retried later instead of failing the capture.
@@ -361,7 +446,8 @@ int fenv_destroy(fenv_t *e) {
         if (e->pend_ev_recorded[k]) (void)hipEventSynchronize(e->pend_ev[k]);
     free_dev(e->device, e->s.px);
     free_dev(e->device, e->pend);
-    pinned_give(e->hpend, e->hpend_dev);
+    pinned_give(e->device, e->hpend, e->hpend_dev);
+    free_host(e->device, e->err_host);
     for (int k = 0; k < 2; ++k) {
         if (e->pend_ev[k]) (void)hipEventDestroy(e->pend_ev[k]);
         if (e->used_ev[k]) (void)hipEventDestroy(e->used_ev[k]);
@@ -388,6 +474,18 @@ int fenv_info(const fenv_t *e, int64_t *o) {
     return FENV_OK;
 }
 
+int fenv_status(const fenv_t *e) {
+    if (!e) return fail(FENV_EINVAL, "fenv_status: NULL handle");
+    return e->stage_check();
+}
+
+void fenv_test_stage_hook(int32_t mode, int32_t n_refills) {
+    g_stage_mode.store(mode);
+    g_stage_n.store(n_refills > 0 ? n_refills : 0);
+}
+
+int64_t fenv_pinned_pool_bytes(int32_t device) { return (int64_t)pinned_cached(device); }
+
 int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::rollout_group_count(e->c) : -1; }
 
 const char *fenv_rollout_kernel(const fenv_t *e, int32_t T) {
@@ -396,12 +494,14 @@ const char *fenv_rollout_kernel(const fenv_t *e, int32_t T) {
 
 int fenv_reset(fenv_t *e, float *obs, void *stream) {
     if (!e) return fail(FENV_EINVAL, "fenv_reset: NULL handle");
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     return e->apply_reset(obs, as_stream(stream));
 }
 
 int fenv_observe(fenv_t *e, float *obs, void *stream) {
     if (!e || !obs) return fail(FENV_EINVAL, "fenv_observe: NULL argument");
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     FENV_HIP(fenvk::launch_reset_observe(e->c, e->s, e->pending(), e->D, false, obs,
                                         as_stream(stream)));
@@ -412,6 +512,7 @@ int fenv_observe(fenv_t *e, float *obs, void *stream) {
 // actions from `act`; else generated in the kernel (gen->offset / gen->out advance per launch).
 static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::ActGen *gen,
                         float *obs, float *rew, uint8_t *done, float *partial, void *stream) {
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     hipStream_t st = as_stream(stream);
     const int64_t A = e->A, D = e->D;
@@ -489,6 +590,7 @@ int fenv_reduce_partials(const float *partial, int64_t count, double *out, void 
 
 int fenv_metrics(fenv_t *e, const float *rew, float *out, double *sums, void *stream) {
     if (!e || !out) return fail(FENV_EINVAL, "fenv_metrics: NULL argument");
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     FENV_HIP(fenvk::launch_metrics(e->c, e->s, e->pending(), e->term_valid, rew, out, sums,
                                    as_stream(stream)));
@@ -498,6 +600,7 @@ int fenv_metrics(fenv_t *e, const float *rew, float *out, double *sums, void *st
 int fenv_get_state(fenv_t *e, float *px, float *py, float *gx, float *gy, int32_t *t,
                    void *stream) {
     if (!e) return fail(FENV_EINVAL, "fenv_get_state: NULL handle");
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     hipStream_t st = as_stream(stream);
     const size_t A = (size_t)e->A, F = (size_t)e->c.F;
@@ -512,6 +615,7 @@ int fenv_get_state(fenv_t *e, float *px, float *py, float *gx, float *gy, int32_
 int fenv_get_state_range(fenv_t *e, int64_t first, int64_t count, float *px, float *py,
                          float *gx, float *gy, int32_t *t, void *stream) {
     if (!e) return fail(FENV_EINVAL, "fenv_get_state_range: NULL handle");
+    if (int rc = e->stage_check()) return rc;
     if (first < 0 || count < 1 || first + count > e->c.F)
         return fail(FENV_EINVAL, "fenv_get_state_range: formations outside the handle's shard");
     FENV_HIP(hipSetDevice(e->device));
@@ -528,6 +632,7 @@ int fenv_get_state_range(fenv_t *e, int64_t first, int64_t count, float *px, flo
 int fenv_metrics_range(fenv_t *e, int64_t first, int64_t count, const float *rew, float *out,
                        double *sums, void *stream) {
     if (!e || !out) return fail(FENV_EINVAL, "fenv_metrics_range: NULL argument");
+    if (int rc = e->stage_check()) return rc;
     if (first < 0 || count < 1 || first + count > e->c.F)
         return fail(FENV_EINVAL, "fenv_metrics_range: formations outside the handle's shard");
     FENV_HIP(hipSetDevice(e->device));
@@ -547,6 +652,7 @@ int fenv_metrics_range(fenv_t *e, int64_t first, int64_t count, const float *rew
 int fenv_set_state(fenv_t *e, const float *px, const float *py, const float *gx, const float *gy,
                    const int32_t *t, void *stream) {
     if (!e || !px || !py || !gx || !gy || !t) return fail(FENV_EINVAL, "fenv_set_state: NULL");
+    if (int rc = e->stage_check()) return rc;
     FENV_HIP(hipSetDevice(e->device));
     hipStream_t st = as_stream(stream);
     const size_t A = (size_t)e->A, F = (size_t)e->c.F;
@@ -617,6 +723,7 @@ int fenv_policy_rollout(fenv_t *e, const float *params, int32_t T, uint64_t seed
                         uint64_t offset, int32_t deterministic, float gamma, float gae_lambda,
                         const fenv_rollout_bufs *bufs, void *stream) {
     if (!e || !params || !bufs) return fail(FENV_EINVAL, "fenv_policy_rollout: NULL argument");
+    if (int rc = e->stage_check()) return rc;
     if (T < 1) return fail(FENV_EINVAL, "fenv_policy_rollout: T must be >= 1");
     const fenv_rollout_bufs &b = *bufs;
     if (!b.obs || !b.action || !b.value || !b.log_prob || !b.reward || !b.episode_start ||

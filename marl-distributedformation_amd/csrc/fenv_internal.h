@@ -2,7 +2,7 @@
 // (fenv_kernels.hip, policy_kernels.hip).  Not installed; the public ABI is include/fenv.h.
 #pragma once
 
-#include <hip/hip_runtime_api.h>
+#include <hip/hip_runtime.h>  // __host__ __device__ for the staged-set tag helpers
 #include <stdint.h>
 
 #include "fenv.h"
@@ -18,18 +18,49 @@ struct DevState {
     uint32_t *ep;    // [F]  episode counter (Philox reset key; not in the reference)
 };
 
-// Reset-side buffers: the host-staged next reset draw set (FENV_RESET_MT19937 mode, same layout
-// as DevState) and the terminal (pre-reset, post-clip) state of the formations reset by their
-// latest done step, which compute_reward_and_done's logged components (simulate.py:183-208) are
-// taken from on a done step (written only on done steps; read by the metrics kernel).
-// Two kernel arguments instead of eight (the step kernels' SGPR budget).
+// Reset-side buffers: the host-staged next reset draw set (FENV_RESET_MT19937 mode) and the
+// terminal (pre-reset, post-clip) state of the formations reset by their latest done step, which
+// compute_reward_and_done's logged components (simulate.py:183-208) are taken from on a done step
+// (written only on done steps; read by the metrics kernel).
+//
+// A staged set is px[A] py[A] gx[F] gy[F] atag[A] gtag[F] (stage_floats): every agent's and every
+// formation's draw carries a tag the host computes from its bits, its index and the set's
+// generation (stage_tag_agent / stage_tag_goal).  The kernels recompute the tag from what they
+// read; a mismatch -- a set read before its copy landed, a stale line, the other slot -- is
+// recorded in the handle's error words (host memory, read by every later API call, which then
+// fails with FENV_ESTATE) instead of being applied silently.
 struct DevPending {
-    const float *pend;  // staged draw set px[A] py[A] gx[F] gy[F] (NULL in Philox mode)
+    const float *pend;  // staged draw set of this launch (NULL in Philox mode)
     float4 *term;       // terminal (px, py, gx, gy)[A] (the goal repeated per agent: one
                         // store, one index)
     float *lf;          // N > kMaxN only: per-agent exchange scratch of the large-formation
                         // kernels (fenv_large.hip), 7 x [A] floats; NULL otherwise
+    uint32_t *err;      // MT19937 mode: the handle's error words [4] (mapped host memory)
+    uint32_t gen;       // generation of the set in `pend` (1 = the ctor's set)
 };
+
+// Tag of one staged draw (host and device compute the same bits; murmur3's 32-bit finaliser).
+__host__ __device__ inline uint32_t stage_mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    return x ^ (x >> 16);
+}
+__host__ __device__ inline uint32_t stage_tag_agent(uint32_t gen, int64_t a, uint32_t bx,
+                                                    uint32_t by) {
+    return stage_mix(bx ^ stage_mix(by ^ stage_mix(gen ^ ((uint32_t)a * 0x9E3779B1u))));
+}
+__host__ __device__ inline uint32_t stage_tag_goal(uint32_t gen, int64_t f, uint32_t bx,
+                                                   uint32_t by) {
+    return stage_mix(bx ^ stage_mix(by ^ stage_mix(gen ^ 0x5BD1E995u ^ ((uint32_t)f * 0x85EBCA6Bu))));
+}
+// floats of one staged set (tags are 32-bit words in float slots)
+inline int64_t stage_floats(int64_t A, int64_t F) { return 3 * A + 3 * F; }
+// error words: [0] kind (0 none; kStageStale: the slot's previous set, two refills back;
+// kStageOther: the set of the other slot; kStageBad: neither), [1] the generation expected,
+// [2] the (shard-local) formation, [3] the number of the launch's lanes that saw it (capped)
+enum : uint32_t { kStageStale = 1, kStageOther = 2, kStageBad = 3 };
 
 struct Consts {
     int64_t F;          // formations in this shard
@@ -91,7 +122,11 @@ hipError_t launch_reset_observe_large(const Consts &c, const DevState &s, const 
                                       int32_t D, bool do_reset, float *obs, hipStream_t st);
 hipError_t launch_metrics_large(const Consts &c, const DevState &s, const DevPending &p,
                                 bool terminal, const float *rew, float *out, hipStream_t st);
-hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, hipStream_t st);
+// delay_sleeps > 0 (test hook fenv_test_stage_hook): every workgroup first waits that many
+// s_sleep 127 periods (~3.4 us each), so a consumer not ordered behind the copy would read the
+// slot's old set
+hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, int32_t delay_sleeps,
+                             hipStream_t st);
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st);
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,

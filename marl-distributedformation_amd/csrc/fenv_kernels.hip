@@ -1031,8 +1031,15 @@ hipError_t launch_reduce_partials(const float *partial, int64_t count, double *o
 // Staged MT19937 reset set: pinned host buffer -> HBM, as a kernel on the launch stream (the
 // refill is then ordered with the rollout kernels by the stream's in-order AQL queue alone; the
 // host buffer is read over the bus through its mapped device address).  n floats, any n.
+// delay > 0: test hook (fenv_test_stage_hook), every workgroup sleeps first.
 __global__ __launch_bounds__(256) void k_stage_copy(float *__restrict__ dst,
-                                                    const float *__restrict__ src, int64_t n) {
+                                                    const float *__restrict__ src, int64_t n,
+                                                    int32_t delay) {
+    if (delay > 0) {
+        if (threadIdx.x == 0)
+            for (int32_t k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(127);
+        __syncthreads();
+    }
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
@@ -1043,11 +1050,13 @@ __global__ __launch_bounds__(256) void k_stage_copy(float *__restrict__ dst,
     if (t < n - 4 * n4) dst[4 * n4 + t] = src[4 * n4 + t];
 }
 
-hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, hipStream_t st) {
+hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, int32_t delay_sleeps,
+                             hipStream_t st) {
     int64_t blocks = (n / 4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n);
+    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n,
+                       delay_sleeps);
     return hipGetLastError();
 }
 

@@ -181,9 +181,15 @@ class FormationEnv(_BASE):
         h = getattr(self, "_h", None)
         self._h = None
         if h is not None and h.value:
-            # finish the work this env queued on the caller's stream before its buffers go
-            torch.cuda.current_stream(self.device).synchronize()
-            _lib.destroy_handle(h)
+            if torch.cuda.is_current_stream_capturing():
+                # inside a HIP graph capture a synchronize would invalidate it: park the handle
+                # (destroyed at the next create / release outside a capture); the torch buffers
+                # below are freed by the caching allocator, which defers reuse past the capture
+                _lib.destroy_handle(h)
+            else:
+                # finish the work this env queued on the caller's stream before its buffers go
+                torch.cuda.current_stream(self.device).synchronize()
+                _lib.destroy_handle(h)
         self._host = None
         for k in ("obs_dev", "rew_dev", "done_dev", "_act_dev"):
             if hasattr(self, k):
@@ -241,6 +247,12 @@ class FormationEnv(_BASE):
         px, py, gx, gy, _ = self._formation_state(0)
         self._fig.update(px, py, gx, gy)
 
+    def check(self) -> None:
+        """Raise FenvError if a launch of this env applied a staged MT19937 reset set that failed
+        its tag check (``fenv_status``; a host read, no GPU call -- call it after a synchronize
+        to cover the launches issued so far).  The numpy faces call it after their copies."""
+        _lib.check(_lib.lib().fenv_status(self._h), "fenv_status")
+
     def info(self) -> dict:
         out = (ctypes.c_int64 * 8)()
         _lib.check(_lib.lib().fenv_info(self._h, out), "fenv_info")
@@ -281,6 +293,7 @@ class FormationEnv(_BASE):
         host["rew"].copy_(self.rew_dev, non_blocking=True)
         host["done"].copy_(self.done_dev, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
+        self.check()
         if self._fig is not None:
             self._refresh_fig()
         return host["obs"].numpy(), host["rew"].numpy(), host["done"].numpy(), self.infos
@@ -314,6 +327,7 @@ class FormationEnv(_BASE):
         host = self._ensure_host()
         host["obs"].copy_(self.obs_dev, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
+        self.check()
         if self._fig is not None:
             self._refresh_fig()
         return host["obs"].numpy()

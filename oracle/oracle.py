@@ -86,6 +86,44 @@ def philox_actions(act_seed: int, step: int, first_agent: int, num_agents: int) 
     return (v.astype(np.float32) * np.float32(2.0 ** -23)).astype(np.float32)
 
 
+PHILOX_RESET_KEY1 = 0x5EEDF00D  # fenv_api.cpp fenv_create: c.key1
+
+
+def philox_reset_draws(seed: int, formations: np.ndarray, num_agents: int,
+                       episodes: np.ndarray):
+    """The reset draw of ``reset_mode="philox"`` (csrc/env_device.h draw_reset, Philox branch)
+    for global formations ``formations`` [k] entering episode ``episodes`` [k] (the formation's
+    episode counter after the reset: 1 for the ctor's reset, +1 per reset since).  Same
+    distributions as the reference's reset (simulate.py:133-143: agents U(0,400) x U(0,100), goal
+    U(60,340) x U(60,540), torch.rand's 24-bit floats), drawn from Philox4x32-10 with key
+    (seed, 0x5EEDF00D) instead of the global MT19937 stream:
+      agent g = f * N + i: counter (g lo, g hi, episode, 'AGNT') -> words x, y -> px, py;
+      formation f:         counter (f lo, f hi, episode, 'GOAL') -> words x, y -> gx, gy.
+    Not a reference behaviour (the reference only has the MT19937 stream, which
+    ``reset_mode="mt19937"`` replays); the build's throughput-mode RNG, restated to check the
+    kernel.  Returns px, py [k * N] and gx, gy [k] (float32, exactly the kernel's roundings:
+    one fp32 multiply, and for the goal one multiply then one add)."""
+    from policy_oracle import _philox
+    M = np.uint64(0xFFFFFFFF)
+    f = np.asarray(formations, np.uint64)
+    ep = np.asarray(episodes, np.uint64) & M
+    N = int(num_agents)
+    key = (int(seed) & 0xFFFFFFFF, PHILOX_RESET_KEY1)
+    g = (f[:, None] * np.uint64(N) + np.arange(N, dtype=np.uint64)).reshape(-1)
+    epa = np.repeat(ep, N)
+    ra = _philox(np.stack([g & M, g >> np.uint64(32), epa, np.full_like(g, 0x41474E54)], 1), key)
+    rg = _philox(np.stack([f & M, f >> np.uint64(32), ep, np.full_like(f, 0x474F414C)], 1), key)
+
+    def u24(w):
+        return (w & np.uint64(0xFFFFFF)).astype(np.float32) * np.float32(2.0 ** -24)
+
+    px = (u24(ra[:, 0]) * np.float32(400.0)).astype(np.float32)
+    py = (u24(ra[:, 1]) * np.float32(100.0)).astype(np.float32)
+    gx = (u24(rg[:, 0]) * np.float32(280.0) + np.float32(60.0)).astype(np.float32)
+    gy = (u24(rg[:, 1]) * np.float32(480.0) + np.float32(60.0)).astype(np.float32)
+    return px, py, gx, gy
+
+
 # ----------------------------------------------------------------------------- MT19937
 def mt_raw(seed: int, n: int, skip: int = 0) -> np.ndarray:
     """Raw 32-bit MT19937 outputs after init_genrand(seed) (== torch.manual_seed stream)."""

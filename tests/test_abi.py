@@ -227,3 +227,14 @@ def test_destroy_null_and_range_args_fail_cleanly(flib):
     assert L.fenv_get_state_range(None, 0, 1, None, None, None, None, None, None) != 0
     assert L.fenv_metrics_range(None, 0, 1, None, None, None, None) != 0
     assert b"NULL" in L.fenv_last_error()
+
+
+def test_destroy_of_unknown_handle_is_refused(flib):
+    """fenv_destroy checks the library's set of live handles, so a pointer
+    that was never created (or was destroyed already) is refused with FENV_EINVAL before any of
+    its memory is read -- here a host buffer full of garbage stands in for a freed handle."""
+    import ctypes
+    L = flib.lib()
+    junk = ctypes.create_string_buffer(b"\xff" * 4096)
+    assert L.fenv_destroy(ctypes.cast(junk, ctypes.c_void_p)) == -1
+    assert b"not a live handle" in L.fenv_last_error()

@@ -235,3 +235,82 @@ def test_beyond_int32_sizes_sampled_vs_oracle(venv, F, N, goal, T):
     assert abs(sums[0] - rsum) <= 1e-5 * max(1.0, abs(rsum)), (sums[0], rsum)
     assert sums[1] == 0.0 and not bool(done.any())
     assert bool((t1 == T).all())
+
+
+def test_bench_workload_staggered_resets_vs_oracle(venv):
+    """the benchmark's own workload -- BASELINE config 3 (1,048,576 x 5),
+    Philox resets, episode phases staggered by bench.stagger_episodes (formation f starts at
+    steps_since_reset f mod 1002, so 1/1002 of the formations reset at every step), one fused
+    10-step launch (k_rollout_wave_rs with non-temporal stores, as timed) -- replayed across the
+    resets.  The sample holds, for every step index j of the launch, formations that reset at j,
+    plus random ones and the grid's ends.  The C oracle steps the GPU's pre-launch state: the
+    done step's reward and done (scored on the pre-reset state) bit for bit; then the reset
+    formations take oracle.philox_reset_draws (episode 3: ctor 1, reset() 2) and the post-reset
+    observation, and every later step, must match bit for bit; the final state too."""
+    import bench
+    from oracle import philox_reset_draws
+    F, N, T, ep_len = 1 << 20, 5, 10, 1002
+    seed = 0
+    env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                             "goal_in_obs": True}, device=DEV, seed=seed, reset_mode="philox")
+    A = F * N
+    env.reset_tensor()
+    bench.stagger_episodes(env, 0)
+    px0, py0, gx0, gy0, t0 = env.get_state()
+    assert env.rollout_kernel_name(T) == "k_rollout_wave_rs"
+    g = torch.Generator(device=DEV).manual_seed(1234)
+    acts = torch.rand((T, A, 2), device=DEV, generator=g) * 2 - 1  # bench.py's action stream
+    part = torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=DEV)
+    obs, rew, done = env.rollout(acts, partial=part)
+    sums = env.reduce_partials(part).cpu().numpy()
+    px1, py1, gx1, gy1, t1 = env.get_state()
+    torch.cuda.synchronize()
+
+    rng = np.random.default_rng(5)
+    resetting = []
+    for j in range(T):  # formations whose pre-step t at step j is max_steps + 1 = 1001
+        cand = np.arange((ep_len - 1 - j) % ep_len, F, ep_len)
+        resetting.append(rng.choice(cand, 40, replace=False))
+    fs = np.unique(np.concatenate(resetting + [rng.choice(F, 1500, replace=False),
+                                               [0, 1, F - 2, F - 1]]))
+    ag = (fs[:, None] * N + np.arange(N)).reshape(-1)
+    agt, fst = torch.from_numpy(ag).to(DEV), torch.from_numpy(fs).to(DEV)
+    ref = COracleEnv(len(fs), N, True, 0)
+    st = [px0[agt].cpu().numpy(), py0[agt].cpu().numpy(), gx0[fst].cpu().numpy(),
+          gy0[fst].cpu().numpy(), t0[fst].cpu().numpy()]
+    ref.set_state(*st)
+    a_s = acts[:, agt].cpu().numpy()
+    o_s, r_s, d_s = obs[:, agt].cpu().numpy(), rew[:, agt].cpu().numpy(), done[:, agt].cpu().numpy()
+    seen = set()
+    for j in range(T):
+        _, rr, rd, _ = ref.step(np.ascontiguousarray(a_s[j]))
+        assert np.array_equal(bits(r_s[j]), bits(rr)), f"reward step {j}"
+        assert np.array_equal(d_s[j], rd), f"done step {j}"
+        dfm = np.nonzero(rd.reshape(-1, N)[:, 0])[0]  # sample-local formations reset at j
+        assert set(resetting[j]) <= set(fs[dfm].tolist()), f"expected resets missing at step {j}"
+        seen.add(j)
+        if dfm.size:  # the oracle drew from its MT19937 stream: put the Philox draw in place
+            px, py, gx, gy, t = ref.get_state()
+            rx, ry, rgx, rgy = philox_reset_draws(seed, fs[dfm], N, np.full(dfm.size, 3))
+            ai = (dfm[:, None] * N + np.arange(N)).reshape(-1)
+            px[ai], py[ai], gx[dfm], gy[dfm] = rx, ry, rgx, rgy
+            assert np.all(t[dfm] == 0)
+            ref.set_state(px, py, gx, gy, t)
+        ro = ref.observe()
+        assert np.array_equal(bits(o_s[j]), bits(ro)), f"obs step {j} (post-reset)"
+    assert seen == set(range(T))
+    rs = ref.get_state()
+    for name, v, w, idx in (("px", px1, rs[0], agt), ("py", py1, rs[1], agt),
+                            ("gx", gx1, rs[2], fst), ("gy", gy1, rs[3], fst),
+                            ("t", t1, rs[4], fst)):
+        assert np.array_equal(bits(v[idx].cpu().numpy()), bits(w)), name
+    # size-independent: every formation reset exactly once in the window iff its phase says so,
+    # and the stats records cover every agent-step
+    tt0 = t0.cpu().numpy().astype(np.int64)
+    want = (tt0 >= ep_len - T)
+    got = done.cpu().numpy().reshape(T, F, N)[:, :, 0].any(0)
+    assert np.array_equal(want, got)
+    assert int(done.sum().item()) == int(want.sum()) * N
+    rsum = rew.double().sum().item()
+    assert abs(sums[0] - rsum) <= 1e-5 * max(1.0, abs(rsum)), (sums[0], rsum)
+    assert sums[1] == float(done.sum().item())

@@ -666,3 +666,32 @@ def test_randomized_shapes_vs_oracle(venv):
                           max_steps=max_steps)
 
     check()
+
+
+def test_philox_reset_draws_match_restatement(venv):
+    """reset_mode="philox": the kernel's reset draws (csrc/env_device.h draw_reset) equal the numpy
+    restatement oracle.philox_reset_draws bit for bit -- the ctor's reset (episode 1), reset()
+    (episode 2) and in-launch auto-resets (episode 3, 4) of a shard [300, 600) of 900 formations,
+    through the role-split, workgroup and large-formation kernels (the staged kernel at full
+    size: tests/test_gpu_fullsize.py)."""
+    from oracle import philox_reset_draws
+    for N, F, first, total in ((5, 300, 300, 900), (64, 40, 7, 60), (100, 9, 3, 20),
+                               (1500, 3, 1, 5)):
+        env = make_env(venv, F, N, True, 77, reset_mode="philox", max_steps=2,
+                       first_formation=first, total_formations=total)
+        fg = np.arange(first, first + F)
+
+        def check(ep, what):
+            px, py, gx, gy, t = (v.cpu().numpy() for v in env.get_state())
+            rx, ry, rgx, rgy = philox_reset_draws(77, fg, N, np.full(F, ep))
+            for a, b, nm in ((px, rx, "px"), (py, ry, "py"), (gx, rgx, "gx"), (gy, rgy, "gy")):
+                assert np.array_equal(bits(a), bits(b)), f"N={N} {what}: {nm}"
+            assert np.all(t == 0)
+
+        check(1, "ctor")
+        env.reset_tensor()
+        check(2, "reset()")
+        # episodes of max_steps + 2 = 4 steps: launches ending on the done steps
+        for ep in (3, 4):
+            env.rollout(torch.zeros((4, F * N, 2), device=DEV))
+            check(ep, f"auto-reset {ep}")
