@@ -164,9 +164,9 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
 // k_rollout_wave_split) gives one formation group two waves that both carry the state (the
 // kinematics, done and auto-reset are recomputed bit-identically by each): kRoleState writes
 // reward / done / the stats sums / the terminal and final state, kRoleObs only the observations.
-// FENV_SPLIT3 splits the observation work once more, by step parity: kRoleObsE writes the
-// observations of the even steps, kRoleObsO those of the odd ones (both still carry the state).
-constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2, kRoleObsE = 3, kRoleObsO = 4;
+// (A third role splitting the observations by step parity measured slower at config 1,
+// profiles/ab/r3_config1_split3_ab.txt; source at commit 2c54623.)
+constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2;
 
 template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll, bool NT = false,
           bool OB = false>
@@ -179,7 +179,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
                                              uint8_t *__restrict__ done, float &rsum,
                                              float &dsum, const RSStage &rsg = RSStage{}) {
     const int64_t A = c.F * (int64_t)c.N;
-    constexpr bool kObsR = ROLE == kRoleObs || ROLE == kRoleObsE || ROLE == kRoleObsO;
+    constexpr bool kObsR = ROLE == kRoleObs;
     Agent s{0.f, 0.f, 0.f, 0.f, 0, 0u};
     if (active) {
         s.px = st.px[a];
@@ -233,14 +233,11 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         env_step<MODE, X, !kObsR>(c, p, x, f, a, i, ac, s, rw, dn, rs);
         any_reset |= rs;
         const int64_t row = (int64_t)k * A + a;
-        // step-parity roles: with an even prefetch depth the parity of k is the ring slot's
-        const int par = (kPF % 2 == 0 ? j : k) & 1;
-        const bool own = ROLE == kRoleObsE ? par == 0 : (ROLE == kRoleObsO ? par == 1 : true);
         if constexpr (OB) {  // obs non-NULL and 16-B aligned (the launcher checks)
             float o[8];
             env_obs<D>(x, s, o);
             store_obs_rows_buf<NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-        } else if (ROLE != kRoleState && obs && own) {
+        } else if (ROLE != kRoleState && obs) {
             float o[8];
             env_obs<D>(x, s, o);
             store_obs_rows<D, NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
@@ -353,10 +350,8 @@ __global__ __launch_bounds__(256) void k_rollout_wave(Consts c, DevState st, Dev
 // formations, so each wave issues about half of a step's instructions and a SIMD holds two
 // waves whose latencies hide each other.  The stats record is the 4 kRoleState waves' sums in
 // k_rollout_wave's order: the same records.
-// OS (FENV_SPLIT3): three waves per formation-wave, the observation role split by step parity
-// (waves 4-7 the even steps' observations, waves 8-11 the odd steps').
-template <int D, int MODE, bool RA, int PF, bool OS = false>
-__global__ __launch_bounds__(OS ? 768 : 512) void k_rollout_wave_split(Consts c, DevState st, DevPending p,
+template <int D, int MODE, bool RA, int PF>
+__global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState st, DevPending p,
                                                             int32_t T,
                                                             const float2 *__restrict__ act,
                                                             ActGen gen, float *__restrict__ obs,
@@ -364,7 +359,7 @@ __global__ __launch_bounds__(OS ? 768 : 512) void k_rollout_wave_split(Consts c,
                                                             uint8_t *__restrict__ done,
                                                             float2 *__restrict__ partial,
                                                             bool accum) {
-    __shared__ __attribute__((aligned(16))) float stage[OS ? 8 : 4][64 * 8];
+    __shared__ __attribute__((aligned(16))) float stage[4][64 * 8];
     __shared__ float2 red[4];
     const int lane = threadIdx.x & 63;
     const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -386,17 +381,9 @@ __global__ __launch_bounds__(OS ? 768 : 512) void k_rollout_wave_split(Consts c,
         rollout_body<D, MODE, RA, false, PF, WaveX, kRoleState>(
             c, st, p, x, active, f, a, i, nullptr, lane, M, f_first * N, T, act, gen, nullptr,
             rew, done, rsum, dsum);
-    else if (!OS)
+    else
         rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObs>(
             c, st, p, x, active, f, a, i, stage[w], lane, M, f_first * N, T, act, gen, obs,
-            nullptr, nullptr, rsum, dsum);
-    else if (w8 < 8)
-        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObsE>(
-            c, st, p, x, active, f, a, i, stage[w8 - 4], lane, M, f_first * N, T, act, gen, obs,
-            nullptr, nullptr, rsum, dsum);
-    else
-        rollout_body<D, MODE, RA, false, PF, WaveX, kRoleObsO>(
-            c, st, p, x, active, f, a, i, stage[w8 - 4], lane, M, f_first * N, T, act, gen, obs,
             nullptr, nullptr, rsum, dsum);
     if (partial) {
         if (w8 < 4) {
@@ -814,9 +801,6 @@ static inline bool use_pf(const Consts &c, int32_t T) {
 #ifndef FENV_SPLIT
 #define FENV_SPLIT 1
 #endif
-#ifndef FENV_SPLIT3
-#define FENV_SPLIT3 0  // measured slower at config 1 (profiles/ab/r3_config1_split3_ab.txt)
-#endif
 static inline bool use_split(const Consts &c) {
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
     return FENV_SPLIT && wave_path(c.N) && waves < FENV_RS_MIN_WAVES;
@@ -876,14 +860,7 @@ static hipError_t rollout_dmn(const Consts &c, const DevState &s, const DevPendi
                                a2, g0, obs, rew, done, p2, accum);
     } else if (use_split(c)) {
         const unsigned blocks = (unsigned)group_count(c);
-        if (FENV_SPLIT3 && use_pf(c, T))
-            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, FENV_SMALL_PF, true>),
-                               dim3(blocks), dim3(768), 0, st, c, s, p, T, a2, g0, obs, rew, done,
-                               p2, accum);
-        else if (FENV_SPLIT3)
-            hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, 1, true>), dim3(blocks),
-                               dim3(768), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
-        else if (use_pf(c, T))
+        if (use_pf(c, T))
             hipLaunchKernelGGL((k_rollout_wave_split<D, MODE, false, FENV_SMALL_PF>), dim3(blocks),
                                dim3(512), 0, st, c, s, p, T, a2, g0, obs, rew, done, p2, accum);
         else
@@ -948,9 +925,7 @@ const char *rollout_kernel_name(const Consts &c, int32_t T) {
     if (large_path(c.N)) return "k_rollout_large";
     if (use_rs(c, T)) return "k_rollout_wave_rs";
     if (use_split(c))
-        return use_pf(c, T) ? (FENV_SPLIT3 ? "k_rollout_wave_split (3 roles, prefetch 4)"
-                                           : "k_rollout_wave_split (prefetch 4)")
-                            : (FENV_SPLIT3 ? "k_rollout_wave_split (3 roles)" : "k_rollout_wave_split");
+        return use_pf(c, T) ? "k_rollout_wave_split (prefetch 4)" : "k_rollout_wave_split";
     if (wave_path(c.N)) return use_pf(c, T) ? "k_rollout_wave (prefetch 4)" : "k_rollout_wave";
     return "k_rollout_block";
 }

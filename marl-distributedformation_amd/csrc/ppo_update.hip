@@ -138,16 +138,9 @@ __device__ __forceinline__ float tanh_u(float x) {
 #ifndef FENV_PPO_TANH_PK
 #define FENV_PPO_TANH_PK 1
 #endif
-// FENV_PPO_TANH_ACC: below |x| = 0.55 the exp form cancels (1 - 2/(1 + e^2x) loses up to
-// 1.4e-3 relative near 0, 1.6e-7 absolute); there an odd polynomial x + x^3 p(x^2) (degree-4 p,
-// a relative-error least-squares fit: <= 0.75 ulp over |x| < 0.55) is used instead, branch-free.
-// Above 0.55 the exp form is within ~3 ulp.  tools/tanh_fit.py derives the coefficients.
-// Off by default: it costs 0.5-0.6 us per minibatch (9.85-9.94 vs 9.26-9.39, same box,
-// profiles/ab/r3_ppo_tanh_ab.txt) and moves the reference-config update no closer to torch than
-// the spread of equally valid summation orders (tests/test_gpu_ppo_dp.py bounds the exp form).
-#ifndef FENV_PPO_TANH_ACC
-#define FENV_PPO_TANH_ACC 0
-#endif
+// (An accurate small-argument tanh -- an odd polynomial below |x| = 0.55, where the exp form
+// loses up to 1.4e-3 relative, 1.6e-7 absolute -- was measured 0.5-0.6 us per minibatch slower
+// and no closer to torch; profiles/ab/r3_ppo_tanh_ab.txt, source at commit 2c54623.)
 __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
 #if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK
     using f2 = float __attribute__((ext_vector_type(2)));
@@ -156,18 +149,7 @@ __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1
     const f2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
     const f2 d = 1.0f + e;
     const f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-    f2 y = 1.0f - 2.0f * r;
-#if FENV_PPO_TANH_ACC
-    const f2 u = x * x;
-    f2 p = (f2)-0.006264324299991131f;
-    p = __builtin_elementwise_fma(p, u, (f2)0.02106410823762417f);
-    p = __builtin_elementwise_fma(p, u, (f2)-0.053850289434194565f);
-    p = __builtin_elementwise_fma(p, u, (f2)0.13332565128803253f);
-    p = __builtin_elementwise_fma(p, u, (f2)-0.33333316445350647f);
-    const f2 ys = __builtin_elementwise_fma(x * u, p, x);
-    y.x = __builtin_fabsf(x0) < 0.55f ? ys.x : y.x;
-    y.y = __builtin_fabsf(x1) < 0.55f ? ys.y : y.y;
-#endif
+    const f2 y = 1.0f - 2.0f * r;
     y0 = y.x;
     y1 = y.y;
 #else
@@ -325,29 +307,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             lp[q] = p < P ? lx(p) : kPadIx;
         }
     }
-    // log_std-derived constants of the loss (FENV_PPO_LOSS_PRE): exp, its square, its log and
-    // the reciprocals, per action component, kept in LDS R[kLS + 5 j + ...] by the thread that
-    // updates log_std_j (at the end of its Adam step), so the loss wave's dependent chain starts
-    // from them instead of computing two expf and two logf per minibatch
-#ifndef FENV_PPO_LOSS_PRE
-#define FENV_PPO_LOSS_PRE 0
-#endif
-    constexpr int kLS = 40;
-    auto ls_consts = [&](int j, float ls) {
-        const float sd = expf(ls);
-        const float var = sd * sd;
-        R[kLS + 5 * j + 0] = var;
-        R[kLS + 5 * j + 1] = logf(sd);  // torch: std.log()
-        R[kLS + 5 * j + 2] = 1.0f / (2.0f * var);
-        R[kLS + 5 * j + 3] = 1.0f / var;
-    };
-    if (FENV_PPO_LOSS_PRE && tid < 2) ls_consts(tid, g.params[L.logstd + tid]);
-    int ls_j = -1;  // the log_std component whose Adam slot this thread owns, if any
-#pragma unroll
-    for (int q = 0; q < KP; ++q) {
-        const int pq = own(q);
-        if (pq >= L.logstd && pq < L.logstd + 2) ls_j = pq - L.logstd;
-    }
     bool partner_lost = false;  // split launch: the other block's norm exchange timed out
     const float lb1 = log2f(hp.beta1), lb2 = log2f(hp.beta2);
     double st_pl = 0.0, st_vl = 0.0, st_el = 0.0, st_cf = 0.0;
@@ -461,14 +420,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #ifndef FENV_PPO_ADAM_PK
 #define FENV_PPO_ADAM_PK 1
 #endif
-#ifndef FENV_PPO_ADAM_PRE
-#define FENV_PPO_ADAM_PRE 0
-#endif
 #ifndef FENV_PPO_ADAM_FMA
 #define FENV_PPO_ADAM_FMA 1
 #endif
-    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && FENV_PPO_ADAM_FMA && !FENV_PPO_ADAM_PRE &&
-                         KP % 2 == 0;
+    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && FENV_PPO_ADAM_FMA && KP % 2 == 0;
     // ceil((64 D + 64) / 256) <= 3 for D <= 8 (4 when packed: slot pairs)
     constexpr int kKA = kAS ? (kPK ? 4 : 3) : KP;
     // dL/dz1 in the other network's H1 half (FENV_PPO_DZ1_SEP, split launch: each block owns
@@ -477,14 +432,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_SEP 1
 #endif
     constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
-#ifndef FENV_PPO_LOSS_DIV
-#define FENV_PPO_LOSS_DIV 0
-#endif
 #ifndef FENV_PPO_LOSS_SPREAD
 #define FENV_PPO_LOSS_SPREAD 1
 #endif
     // split launch: the loss wave writes per-sample terms; waves 1-3 take the sums afterwards
-    constexpr bool kSpread = SPLIT && FENV_PPO_LOSS_SPREAD && !FENV_PPO_LOSS_PRE;
+    constexpr bool kSpread = SPLIT && FENV_PPO_LOSS_SPREAD;
     const int stat_tid = kSpread ? 64 : 0;  // the thread accumulating the loss statistics
 #ifndef FENV_PPO_B2_HG
 #define FENV_PPO_B2_HG 1  // split: the b2 gradient summed by the head-gradient phase's lanes
@@ -494,9 +446,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #endif
     constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
     constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
-#ifndef FENV_PPO_SCHED_PIN
-#define FENV_PPO_SCHED_PIN 0
-#endif
 #ifndef FENV_PPO_POST_FIRST
 #define FENV_PPO_POST_FIRST 1
 #endif
@@ -507,30 +456,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #ifndef FENV_PPO_HEADS_K16
 #define FENV_PPO_HEADS_K16 1
 #endif
-#ifndef FENV_PPO_SUMS_W2
-#define FENV_PPO_SUMS_W2 0
-#endif
-    constexpr bool kSW2 = kSpread && FENV_PPO_SUMS_W2;
-#ifndef FENV_PPO_LS_EARLY
-#define FENV_PPO_LS_EARLY 0
-#endif
-#ifndef FENV_PPO_LS_L2
-#define FENV_PPO_LS_L2 0
-#endif
-    constexpr bool kLL2 = FENV_PPO_LS_L2 && !FENV_PPO_LOSS_PRE && !FENV_PPO_LS_EARLY;
 #ifndef FENV_PPO_DZ1_PRE
 #define FENV_PPO_DZ1_PRE 1
 #endif
-#ifndef FENV_PPO_HW_EARLY
-#define FENV_PPO_HW_EARLY 0
-#endif
     constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
-    constexpr bool kHWE = SPLIT && FENV_PPO_HW_EARLY;
-#ifndef FENV_PPO_L2ROWS
-#define FENV_PPO_L2ROWS 0  // measured neutral-to-slower (profiles/ab/r3_ppo_l2rows_ab.txt)
-#endif
-    constexpr bool kL2R = SPLIT && FENV_PPO_L2ROWS && !FENV_PPO_LS_L2 && !FENV_PPO_HW_EARLY &&
-                          !FENV_PPO_LS_EARLY;
 #ifndef FENV_PPO_COEF_FAST
 #define FENV_PPO_COEF_FAST 1
 #endif
@@ -540,24 +469,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #ifndef FENV_PPO_BC_WAVE
 #define FENV_PPO_BC_WAVE 1
 #endif
-    constexpr bool kBCW = SPLIT && !GRAD && FENV_PPO_BC_WAVE && !FENV_PPO_ADAM_PRE;
+    constexpr bool kBCW = SPLIT && !GRAD && FENV_PPO_BC_WAVE;
     constexpr int kBC = 60;  // R slots: this minibatch's Adam step size and 1 / sqrt(bc2)
 #ifndef FENV_PPO_HG_VEC
 #define FENV_PPO_HG_VEC 1
 #endif
-#ifndef FENV_PPO_LS_EARLY
-#define FENV_PPO_LS_EARLY 0
-#endif
-    constexpr bool kLE = FENV_PPO_LS_EARLY && !FENV_PPO_LOSS_PRE;
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
-#ifndef FENV_PPO_ADAM_PRE
-#define FENV_PPO_ADAM_PRE 0
-#endif
-    constexpr bool kAP = SPLIT && !GRAD && FENV_PPO_ADAM_PRE;
-#ifndef FENV_PPO_EARLY_X
-#define FENV_PPO_EARLY_X 0
-#endif
 #ifndef FENV_PPO_ADAM_FMA
 #define FENV_PPO_ADAM_FMA 1
 #endif
@@ -568,13 +486,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         if (p < P) {
             const int ix = SPLIT ? lp[q] : lx(p);
             const float gr = (SPLIT ? gq[q] : G[ix]) * a_coef;
-            if constexpr (kAP) {  // m, v already hold beta1 m, beta2 v (adam_pre)
-                m[q] = __builtin_fmaf(1.0f - hp.beta1, gr, m[q]);
-                v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q]);
-                const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v[q]), a_ib, hp.eps);
-                W[ix] = __builtin_fmaf(-a_ss, m[q] * __builtin_amdgcn_rcpf(den), wq[q]);
-                return;
-            }
 #if FENV_PPO_ADAM_FMA
             m[q] = __builtin_fmaf(1.0f - hp.beta1, gr - m[q], m[q]);
             v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q] * hp.beta2);
@@ -627,25 +538,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             for (int q = q0; q < q1; ++q) adam_slot(q);
         }
     };
-    // kAP: the coefficient-free half of Adam (decayed moments, bias corrections) while the norm
-    // exchange is in flight
-    auto adam_pre = [&]() {
-        step += 1.0f;
-        const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
-        const float bc2 = 1.0f - exp2f(step * lb2);
-        a_ss = hp.lr / bc1;
-        a_ib = 1.0f / __builtin_sqrtf(bc2);
-#pragma unroll
-        for (int q = 0; q < KP; ++q) {
-            m[q] = hp.beta1 * m[q];
-            v[q] = hp.beta2 * v[q];
-        }
-    };
     // the deferred slots of the previous minibatch's Adam step (kAS)
     auto adam_rest = [&]() {
         adam_slots(std::integral_constant<int, kKA>{}, std::integral_constant<int, KP>{});
-        // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
-        if (FENV_PPO_LOSS_PRE && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
     };
     int64_t kmb = 0;
     for (int ep = 0; ep < g.n_epochs; ++ep) {
@@ -654,15 +549,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // loss means: over this minibatch, or (gradient mode) over the global minibatch
             const float invB = GRAD ? g.inv_bg : 1.0f / (float)B;
             float gss = 0.f;  // sum of squares of the gradient entries this thread writes
-            // split: the partner's exchange word read ahead of this block's own post
-            // (FENV_PPO_EARLY_X 1: before the norm's wave sum, 2: before the W1 gradients); the
-            // actor usually arrives after the critic has posted, so its wait starts resolved
-            uint64_t o_early = 0;
-            auto early_load = [&]() {
-                if (SPLIT && !GRAD && tid == 0 && !partner_lost)
-                    o_early = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
             // ---- gather the minibatch (from the prefetch registers), then start the next one
             // (late gather: this minibatch's rows were stored at the end of the previous one)
             if (!kLate || kmb == 0) gather_store(B, (SPLIT && net_b == 0) ? adv_nx : ps[3]);
@@ -688,8 +574,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int w1 = (net ? L.vf0W : L.pi0W) + j * D + q;
                 const float b0 = W[lx(w1)], b1 = W[lx(w1 + 4)];
                 const float bias = W[lx((net ? L.vf0b : L.pi0b) + j)];
-                // the 4 tiles' observation operands read up front (FENV_PPO_SCHED_PIN: kept
-                // ahead of the MFMAs, one LDS wait for the phase instead of one per tile)
+                // the 4 tiles' observation operands read up front (one LDS wait for the phase
+                // instead of one per tile)
                 float oa[4], ob[4];
 #pragma unroll
                 for (int bt = 0; bt < 4; ++bt) {
@@ -697,7 +583,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     oa[bt] = o[0];
                     ob[bt] = o[4];
                 }
-                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int bt = 0; bt < 4; ++bt) {
                     f32x4 acc = {bias, bias, bias, bias};
@@ -723,9 +608,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(1);
-            // The loss's log_std-derived constants (FENV_PPO_LS_EARLY) are computed here, under the
-            // head MFMAs, by every wave (wave 0 keeps them for the loss phase): log_std was final
-            // at the layer-1 barrier, and the loss wave's chain then starts from the samples.
+            // the loss's log_std-derived constants (computed by the loss wave)
             float lc_var0 = 0.f, lc_var1 = 0.f, lc_lsd0 = 0.f, lc_lsd1 = 0.f;
             float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
             auto loss_consts = [&]() {
@@ -757,89 +640,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 lc_iv1 = 1.0f / lc_var1;
 #endif
             };
-            float hwv[16];  // kHWE: the heads' weight operands, read during layer 2
-            if constexpr (kL2R) {
-            // ---- layer 2 by rows (FENV_PPO_L2ROWS, split launch): wave wl = samples
-            // 16 wl .. +15 x all 64 hidden units, as four 16 x 16 tiles on v_mfma_f32_16x16x4f32
-            // (K-step s of lane group q <-> hidden input 16 q + s: conflict-free operand reads;
-            // the A operand is shared by the four tiles).  With whole rows in the wave, the heads
-            // mu = actW . h2 + actb / value = valW . h2 + valb are per-lane products over its 4
-            // columns and a 16-lane DPP row sum: no heads phase, no barrier, no H2 re-read.
-            {
-                const int net = w >> 2, bt = wl, q = lane >> 4, c = lane & 15;
-                const float *Ar = H1 + (net * kPB + 16 * bt + c) * kRow + 16 * q;
-                const float *Bw = W + lx(net ? L.vf2W : L.pi2W) + c * kRow + 16 * q;
-                f32x4 acc[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float bias = W[lx((net ? L.vf2b : L.pi2b) + 16 * t + c)];
-                    acc[t] = f32x4{bias, bias, bias, bias};
-                }
-                // operands read up front (the scheduler otherwise sinks each step's reads to
-                // their MFMAs, exposing the LDS latency once per step)
-                float av[16], bv[4][16];
-#pragma unroll
-                for (int s4 = 0; s4 < 16; ++s4) {
-                    av[s4] = Ar[s4];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) bv[t][s4] = Bw[16 * t * kRow + s4];
-                }
-#pragma unroll
-                for (int s4 = 0; s4 < 16; ++s4)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[t][s4], acc[t],
-                                                                     0, 0, 0);
-                // tanh, H2 rows (kept for the backward), and the heads' per-lane partials
-                const int hw0 = net ? L.valW : L.actW;
-                float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
-                float *Hr = H2 + (net * kPB + 16 * bt + 4 * q) * kRow + c;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float wa = W[lx(hw0 + 16 * t + c)];
-                    // branch-free: the critic reads its own row twice and drops the second sum
-                    const float wb = W[lx(net ? hw0 + 16 * t + c : L.actW + kHid + 16 * t + c)];
-#pragma unroll
-                    for (int r = 0; r < 4; r += 2) {
-                        float y0, y1;
-                        tanh_u2(acc[t][r], acc[t][r + 1], y0, y1);
-                        Hr[r * kRow + 16 * t] = y0;
-                        Hr[(r + 1) * kRow + 16 * t] = y1;
-                        p0[r] = __builtin_fmaf(wa, y0, p0[r]);
-                        p0[r + 1] = __builtin_fmaf(wa, y1, p0[r + 1]);
-                        p1[r] = __builtin_fmaf(wb, y0, p1[r]);
-                        p1[r + 1] = __builtin_fmaf(wb, y1, p1[r + 1]);
-                    }
-                }
-                // sum over the 16 lanes of each row (hidden 16 t + c): lane 15 of the row holds it
-                auto rsum16 = [](float v) {
-                    int x = __float_as_int(v);
-                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
-                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
-                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false)));
-                    x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false)));
-                    return __int_as_float(x);
-                };
-                float m0[4], m1[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    m0[r] = rsum16(p0[r]);
-                    m1[r] = rsum16(p1[r]);
-                }
-                if (c == 15) {
-                    const float hb0 = W[lx(net ? L.valb : L.actb)];
-                    float *s0 = S + (net ? sVAL : sMU0) * kPB + 16 * bt + 4 * q;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s0[r] = m0[r] + hb0;
-                    if (!net) {
-                        const float hb1 = W[lx(L.actb + 1)];
-                        float *s1 = S + sMU1 * kPB + 16 * bt + 4 * q;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) s1[r] = m1[r] + hb1;
-                    }
-                }
-            }
-            } else {
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
             // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
@@ -849,13 +649,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *Ar = H1 + (net * kPB + 32 * mt + c) * kRow + 32 * h;
                 const float *Bc = W + lx(net ? L.vf2W : L.pi2W) + (32 * nt + c) * kRow + 32 * h;
                 const float bias = W[lx((net ? L.vf2b : L.pi2b) + 32 * nt + c)];
-                if constexpr (kHWE) {  // the heads' weight operands (independent of layer 2)
-                    const int hq = lane >> 4, hc = lane & 15;
-                    const int hw = net ? L.valW : L.actW + (hc & 1) * kHid;
-#pragma unroll
-                    for (int s4 = 0; s4 < 16; ++s4)
-                        hwv[s4] = W[lx(hw + (FENV_PPO_HEADS_K16 ? 16 * hq + s4 : 4 * s4 + hq))];
-                }
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
@@ -867,11 +660,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     ra[j] = Ar[j];
                     rb[j] = Bc[j];
                 }
-                // FENV_PPO_SCHED_PIN: keep the ring's loads ahead of the MFMAs (the scheduler
-                // otherwise sinks them to their uses: an LDS round trip per MFMA pair)
-                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
-                // kLL2: the loss constants in the shadow of the 32 MFMAs (every wave, branch-free)
-                if (kLL2) loss_consts();
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RL) {
 #pragma unroll
@@ -901,7 +689,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
             // v_mfma_f32_16x16x4f32: wave w = net w>>2, samples 16(w&3)..+15, output columns 0..15
             // of which 2 (actor) / 1 (critic) are real; K = 64 hidden as 16 MFMAs
-            if (kLE) loss_consts();
             {
                 const int net = w >> 2, bt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
@@ -916,7 +703,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     for (int s4 = 0; s4 < 16; ++s4) {
                         const int kk = FENV_PPO_HEADS_K16 ? 16 * q + s4 : 4 * s4 + q;
                         av[s4] = a[kk - q];
-                        wv[s4] = kHWE ? hwv[s4] : W[lx(hw + kk)];
+                        wv[s4] = W[lx(hw + kk)];
                     }
                     f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};  // kAcc2: two chains (even / odd steps)
 #pragma unroll
@@ -944,7 +731,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     for (int r = 0; r < 4; ++r) so[r] = acc[r] + hb;
                 }
             }
-            }  // !kL2R
             __syncthreads();
             FENV_PPO_PHASE(2);
             // ---- heads, losses and per-sample gradients (wave 0, lane = sample; split: wave 0 of
@@ -953,18 +739,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if (wl == 0) {
                 const bool do_pi = !SPLIT || net_b == 0, do_vf = !SPLIT || net_b == 1;
                 const bool on = lane < B;
-#if FENV_PPO_LOSS_PRE
-                const float var0 = R[kLS + 0], lsd0 = R[kLS + 1], i2v0 = R[kLS + 2], iv0 = R[kLS + 3];
-                const float var1 = R[kLS + 5], lsd1 = R[kLS + 6], i2v1 = R[kLS + 7], iv1 = R[kLS + 8];
-                (void)var0;
-                (void)var1;
-#else
-                if (!kLE && !kLL2 && (!kSpread || do_pi)) loss_consts();
+                if (!kSpread || do_pi) loss_consts();
                 const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
-                const float iv0 = lc_iv0, iv1 = lc_iv1, var0 = lc_var0, var1 = lc_var1;
-                (void)var0;
-                (void)var1;
-#endif
+                const float iv0 = lc_iv0, iv1 = lc_iv1;
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
                 if constexpr (kSpread) {
@@ -976,13 +753,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                             const float mu0 = S[sMU0 * kPB + lane], mu1 = S[sMU1 * kPB + lane];
                             const float a0 = S[sA0 * kPB + lane], a1 = S[sA1 * kPB + lane];
                             const float d0 = a0 - mu0, d1 = a1 - mu1;
-#if FENV_PPO_LOSS_DIV  // torch's divisions (correctly rounded), not reciprocal products
-                            const float lp = (-(d0 * d0) / (2.0f * var0) - lsd0 - kLogSqrt2Pi) +
-                                             (-(d1 * d1) / (2.0f * var1) - lsd1 - kLogSqrt2Pi);
-#else
                             const float lp = (-(d0 * d0) * i2v0 - lsd0 - kLogSqrt2Pi) +
                                              (-(d1 * d1) * i2v1 - lsd1 - kLogSqrt2Pi);
-#endif
                             const float ratio = expf(lp - S[sOLP * kPB + lane]);
                             const float an = S[sADV * kPB + lane];
                             const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
@@ -995,17 +767,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                             const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
                             const float dratio = -(g1 * an + g2 * an * inside) * invB;
                             const float dlp = dratio * ratio;
-#if FENV_PPO_LOSS_DIV
-                            gmu0 = dlp * (d0 / var0);
-                            gmu1 = dlp * (d1 / var1);
-                            gls0 = dlp * ((d0 * d0) / var0 - 1.0f);
-                            gls1 = dlp * ((d1 * d1) / var1 - 1.0f);
-#else
                             gmu0 = dlp * (d0 * iv0);
                             gmu1 = dlp * (d1 * iv1);
                             gls0 = dlp * ((d0 * d0) * iv0 - 1.0f);
                             gls1 = dlp * ((d1 * d1) * iv1 - 1.0f);
-#endif
                         }
                         S[sGMU0 * kPB + lane] = gmu0;
                         S[sGMU1 * kPB + lane] = gmu1;
@@ -1110,9 +875,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             __syncthreads();
             FENV_PPO_PHASE(3);
             // kSpread: the loss sums, one or two per wave of waves 1-3 (wave 0 just ran the loss);
-            // their outputs are only read from the norm phase on (kSW2: taken in the shadow of
-            // the W2-gradient MFMAs instead, below)
-            // FENV_PPO_SUMS_LATE: after this phase's head-gradient / dL/dz2 work instead of before
+            // their outputs are only read from the norm phase on
             auto loss_sums = [&]() {
                 if (net_b == 0) {
                     if (wl == 1) {
@@ -1154,10 +917,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     }
                 }
             };
-#ifndef FENV_PPO_SUMS_LATE
-#define FENV_PPO_SUMS_LATE 0  // measured neutral (profiles/ab/r3_ppo_sums_late_ab.txt)
-#endif
-            if constexpr (kSpread && !kSW2 && !FENV_PPO_SUMS_LATE) loss_sums();
+            if constexpr (kSpread) loss_sums();
             // ---- head weight gradients on v_mfma_f32_16x16x4f32 (wave w = net w>>2, hidden rows
             // 16(w&3)..+15, columns gmu0/gmu1 resp. gv; K = 64 samples as 16 MFMAs), then
             // dL/dz2 in place over the SAME H2 columns (only this wave reads or writes them in
@@ -1244,7 +1004,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         gss = __builtin_fmaf(acc[r], acc[r], gss);
                     }
                 }
-                if constexpr (kSpread && !kSW2 && FENV_PPO_SUMS_LATE) loss_sums();
             } else {
                 const int net = w >> 2, kt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
@@ -1324,26 +1083,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     rc[j] = pc[j];
                     rd[j] = pd[j * kRow];
                 }
-                // FENV_PPO_SCHED_PIN: loads ahead, and the two chains interleaved (the scheduler
-                // otherwise runs them one after the other with an LDS round trip per pair)
-                if (FENV_PPO_SCHED_PIN) __builtin_amdgcn_sched_barrier(0);
-                // kSW2: this wave's two loss sums (slots by block and wave; wave 0 a dummy pair),
-                // branch-free so they issue between the MFMAs
-                float ls1 = 0.f, ls2 = 0.f;
-                if constexpr (kSW2) {
-                    constexpr int kT1[8] = {sPL, sPL, sGL0, sGMU0, sVLS, sVLS, sGV, sGV};
-                    constexpr int kT2[8] = {sPL, sCF, sGL1, sGMU1, sVLS, sVLS, sGV, sGV};
-                    const int ix = 4 * net_b + wl;
-                    ls1 = wsum(S[kT1[ix] * kPB + lane]);
-                    ls2 = wsum(S[kT2[ix] * kPB + lane]);
-                }
 #pragma unroll
                 for (int i0 = 0; i0 < 32; i0 += RD) {
 #pragma unroll
                     for (int j = 0; j < RD; ++j) {
                         gw = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], gw, 0, 0, 0);
                         dz = __builtin_amdgcn_mfma_f32_32x32x2f32(rc[j], rd[j], dz, 0, 0, 0);
-                        if (FENV_PPO_SCHED_PIN == 2) __builtin_amdgcn_sched_barrier(0);
                         const int i = i0 + RD + j;
                         if (i < 32) {
                             ra[j] = pa[i * kRow];
@@ -1364,36 +1109,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                                              0, 0, 0);
                 }
 #endif
-                if constexpr (kSW2) {  // the lane-0 stores of the loss sums
-                    if (lane == 0) {
-                        if (net_b == 0) {
-                            if (wl == 1) {
-                                st_pl += (double)(-ls1 * invB);
-                                if (!GRAD || g.ent_once) st_el += (double)(-R[kEnt]);
-                                st_cf += (double)(ls2 * invB);
-                            } else if (wl == 2) {
-                                // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef; gradient
-                                // mode: the entropy term once over the ranks (ent_once)
-                                const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
-                                const float g0 = ls1 - ec, g1 = ls2 - ec;
-                                G[lx(L.logstd)] = g0;
-                                G[lx(L.logstd + 1)] = g1;
-                                gss += g0 * g0 + g1 * g1;
-                            } else if (wl == 3) {
-                                G[lx(L.actb)] = ls1;
-                                G[lx(L.actb + 1)] = ls2;
-                                gss += ls1 * ls1 + ls2 * ls2;
-                            }
-                        } else {
-                            if (wl == 1) {
-                                st_vl += (double)(ls1 * invB);
-                            } else if (wl == 2) {
-                                G[lx(L.valb)] = ls1;
-                                gss += ls1 * ls1;
-                            }
-                        }
-                    }
-                }
                 float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -1428,7 +1143,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(7);
-            if (FENV_PPO_EARLY_X == 2) early_load();
             // ---- W1 gradients GW1 = dZ1^T . O on v_mfma_f32_16x16x4f32 (wave w: net w>>2, hidden
             // rows 16(w&3)..+15, obs columns 0..15 of which 0..D-1 are real; K = 64 samples,
             // slot q <-> sample 16q + i) and b1 gradients
@@ -1493,7 +1207,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- clip_grad_norm_(max_grad_norm): global 2-norm from the squares each thread
             // accumulated as it wrote its gradient entries (every entry is written exactly once
             // per minibatch), one wave sum each, reduced after the barrier
-            if (FENV_PPO_EARLY_X == 1) early_load();
             gss = wsum(gss);
             if (lane == 0) R[wl] = gss;
             __syncthreads();
@@ -1531,11 +1244,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                        (seq << 32) | __float_as_uint(tot), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     if (!partner_lost) {
-                        if (FENV_PPO_EARLY_X && (o_early >> 32) == seq)
-                            o = o_early;
-                        else
-                            o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        o = __hip_atomic_load(g.xch + 2 * (net_b ^ 1) + (kmb & 1),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
                 if (FENV_PPO_POST_FIRST) read_gw();
@@ -1552,7 +1262,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                      net_b == 0 ? adv_nx : ps[3]);
                     }
                 }
-                if constexpr (kAP) adam_pre();
                 if (tid == 0) {
                     // after one timed-out wait the partner is taken as lost for good: no further
                     // waits, so a broken launch ends in milliseconds, not one timeout per
@@ -1587,7 +1296,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 step += 1.0f;
                 a_ss = R[kBC];
                 a_ib = R[kBC + 1];
-            } else if constexpr (!kAP) {
+            } else {
                 step += 1.0f;
                 const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
                 const float bc2 = 1.0f - exp2f(step * lb2);
@@ -1596,8 +1305,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             // kAS: slots 0..kKA-1 (layer 1) now, the rest in the next minibatch's layer-1 phase
             adam_slots(std::integral_constant<int, 0>{}, std::integral_constant<int, kKA>{});
-            // the owner of log_std_j refreshes the loss constants (its own LDS write, re-read)
-            if (!kAS && FENV_PPO_LOSS_PRE && !GRAD && ls_j >= 0) ls_consts(ls_j, W[lx(L.logstd + ls_j)]);
             __syncthreads();
             FENV_PPO_PHASE(10);
         }

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4, first GPU job: the new staging / Philox / lifecycle tests, then the parity file.
+# Round 4, first GPU job: the new staging / Philox / lifecycle tests, then the PPO log_std probe.
 set -o pipefail
-mkdir -p gpurun_out/r4a
 cd "$(dirname "$0")/.."
+mkdir -p gpurun_out/r4a
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_gpu_lifecycle.py \
   "tests/test_gpu_parity.py::test_philox_reset_draws_match_restatement" \
@@ -11,4 +11,8 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   > gpurun_out/r4a/pytest_new.log 2>&1
 rc=$?
 tail -30 gpurun_out/r4a/pytest_new.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u tools/ppo_logstd_probe.py > gpurun_out/r4a/ppo_logstd_probe.json 2> gpurun_out/r4a/ppo_logstd_probe.err
+rc=$?
+tail -60 gpurun_out/r4a/ppo_logstd_probe.json
 exit $rc
