@@ -35,7 +35,8 @@ extern "C" {
  *   1  round-1/2 entry points (policy_forward with row0)
  *   2  + fenv_abi_version, fenv_get_state_range, fenv_metrics_range, ppo_workspace_bytes,
  *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject
- *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes (no signature changed) */
+ *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes, fenv_debug_staging (no
+ *        signature changed) */
 #define FENV_ABI_VERSION 3
 int fenv_abi_version(void);
 
@@ -99,6 +100,13 @@ void fenv_test_stage_hook(int32_t mode, int32_t n_refills);
 /* Bytes of pinned staging buffers cached for reuse on `device` (bounded at 512 MiB per device;
  * a destroyed env's buffer is freed instead when the pool is full). */
 int64_t fenv_pinned_pool_bytes(int32_t device);
+
+/* Diagnostic (synchronous): info_host[0..9] = {slot the next reset reads, generation of slot 0,
+ * of slot 1, floats per staged set, error words 0..2, next generation, device address of the
+ * terminal-state records, of the staged sets}; with out_host (floats per
+ * staged set) the staged set of device slot `which` (0, 1) or of host slot which - 2 (2, 3);
+ * which = 4: the terminal-state records (px, py, gx, gy)[A] (4 A floats; any reset mode). */
+int fenv_debug_staging(fenv_t *env, int32_t which, float *out_host, int64_t *info_host);
 
 /* out_host[0..7] = {num_formation, num_agents, obs_dim, num_agents_total(A), steps_since_reset
  * (common value, -1 if formations differ), reset_mode, first_formation, total_formations}. */

@@ -70,6 +70,7 @@ SIGNATURES = {
     "fenv_status": (_I32, [_P]),
     "fenv_test_stage_hook": (None, [_I32, _I32]),
     "fenv_pinned_pool_bytes": (_I64, [_I32]),
+    "fenv_debug_staging": (_I32, [_P, _I32, _P, _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
 

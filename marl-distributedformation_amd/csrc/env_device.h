@@ -69,7 +69,7 @@ __device__ __forceinline__ float u24(uint32_t r) { return (float)(r & 0xFFFFFFu)
 // A staged MT19937 draw failed its tag check (fenv_internal.h DevPending): classify it against the
 // generations the slot and the other slot held, and record it in the handle's error words (host
 // memory; relaxed system-scope vector stores -- any lane's values will do).
-static __device__ __attribute__((noinline)) void stage_tag_fail(const DevPending &p, int64_t f, int64_t a,
+__device__ __forceinline__ void stage_tag_fail(const DevPending &p, int64_t f, int64_t a,
                                                          uint32_t tag, uint32_t bx, uint32_t by) {
     uint32_t kind = kStageBad;
     if (tag == stage_tag_agent(p.gen - 2u, a, bx, by)) kind = kStageStale;
@@ -92,13 +92,17 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
         py = p.pend[A + a];
         gx = p.pend[2 * A + f];
         gy = p.pend[2 * A + c.F + f];
-        const uint32_t *tg = reinterpret_cast<const uint32_t *>(p.pend + 2 * A + 2 * c.F);
-        const uint32_t ta = tg[a], tf = tg[A + f];
-        const uint32_t bx = __float_as_uint(px), by = __float_as_uint(py);
-        if (ta != stage_tag_agent(p.gen, a, bx, by))
-            stage_tag_fail(p, f, a, ta, bx, by);
-        else if (tf != stage_tag_goal(p.gen, f, __float_as_uint(gx), __float_as_uint(gy)))
-            stage_tag_fail(p, f, a, 0u, 0u, 0u);  // the goal's tag: kStageBad
+        // the tags of the lane's draws (a lane owning no agent -- env_step's `live` -- may index
+        // past the set; it applies nothing, so it is not checked there)
+        if (f < c.F && a < A) {
+            const uint32_t *tg = reinterpret_cast<const uint32_t *>(p.pend + 2 * A + 2 * c.F);
+            const uint32_t ta = tg[a], tf = tg[A + f];
+            const uint32_t bx = __float_as_uint(px), by = __float_as_uint(py);
+            if (ta != stage_tag_agent(p.gen, a, bx, by))
+                stage_tag_fail(p, f, a, ta, bx, by);
+            else if (tf != stage_tag_goal(p.gen, f, __float_as_uint(gx), __float_as_uint(gy)))
+                stage_tag_fail(p, f, a, 0u, 0u, 0u);  // the goal's tag: kStageBad
+        }
     } else {
         const uint64_t fg = (uint64_t)(c.f0 + f);
         const uint64_t ag = fg * (uint64_t)c.N + (uint64_t)i;
@@ -206,10 +210,17 @@ struct Agent {
 // FormationSimulator.step (simulate.py:70-118) for this lane's agent.  Returns the reward
 // (pre-reset state) and done; leaves the post-(auto-)reset state in `s`.
 // TERM = false: leave the terminal-state record to another wave (the split kernel's kRoleState).
+// live = false: a lane that owns no agent (the grid's padding, a wave's lanes past its last
+// whole formation, a workgroup's threads past N).  It still runs the step -- the ring exchanges
+// are wave-wide -- from a zero state whose steps_since_reset starts at 0 every launch, so it has
+// a phantom done step max_steps + 1 steps into a launch.  It must store nothing there: its
+// (f, a) index a formation that is not its own, or none (the round-2/3
+// post-reset failures were these lanes' terminal-state stores of zeros, past the end of the
+// terminal buffer into the staged reset set that follows it in memory).
 template <int MODE, class X, bool TERM = true>
 __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, const X &x,
-                                         int64_t f, int64_t a, int i, float2 act, Agent &s,
-                                         float &rw, bool &dn, bool &did_reset) {
+                                         int64_t f, int64_t a, int i, bool live, float2 act,
+                                         Agent &s, float &rw, bool &dn, bool &did_reset) {
     // vectorized_env.py:69-70 (v = 10 * a), simulate.py:82 (agents += v)
     const float x1 = s.px + 10.0f * act.x;
     const float y1 = s.py + 10.0f * act.y;
@@ -251,7 +262,7 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
         // (simulate.py:183-208) describe it, not the freshly drawn one
         // (indices laundered inside the branch: otherwise the compiler hoists these rarely used
         // addresses out of the step loop into 4 loop-invariant VGPRs)
-        if (TERM) {
+        if (TERM && live) {
             int64_t ta = a;
             asm volatile("" : "+v"(ta));
             p.term[ta] = make_float4(s.px, s.py, s.gx, s.gy);

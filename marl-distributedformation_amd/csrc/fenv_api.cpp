@@ -486,6 +486,34 @@ void fenv_test_stage_hook(int32_t mode, int32_t n_refills) {
 
 int64_t fenv_pinned_pool_bytes(int32_t device) { return (int64_t)pinned_cached(device); }
 
+int fenv_debug_staging(fenv_t *e, int32_t which, float *out_host, int64_t *info_host) {
+    if (!e || !info_host) return fail(FENV_EINVAL, "fenv_debug_staging: NULL argument");
+    info_host[0] = e->rd;
+    info_host[1] = e->slot_gen[0];
+    info_host[2] = e->slot_gen[1];
+    info_host[3] = (int64_t)e->pend_floats();
+    info_host[4] = e->err_host ? e->err_host[0] : 0;
+    info_host[5] = e->err_host ? e->err_host[1] : 0;
+    info_host[6] = e->err_host ? e->err_host[2] : 0;
+    info_host[7] = e->gen_next;
+    info_host[8] = (int64_t)reinterpret_cast<uintptr_t>(e->term);
+    info_host[9] = (int64_t)reinterpret_cast<uintptr_t>(e->pend);
+    if (out_host && which == 4) {  // the terminal-state records (px, py, gx, gy)[A]
+        FENV_HIP(hipSetDevice(e->device));
+        FENV_HIP(hipDeviceSynchronize());
+        FENV_HIP(hipMemcpy(out_host, e->term, (size_t)e->A * 16, hipMemcpyDeviceToHost));
+        return FENV_OK;
+    }
+    if (!out_host || !e->pend || which < 0 || which > 3) return FENV_OK;
+    FENV_HIP(hipSetDevice(e->device));
+    const size_t off = (size_t)(which & 1) * e->pend_stride();
+    if (which < 2)
+        FENV_HIP(hipMemcpy(out_host, e->pend + off, e->pend_floats() * 4, hipMemcpyDeviceToHost));
+    else
+        std::memcpy(out_host, e->hpend + off, e->pend_floats() * 4);
+    return FENV_OK;
+}
+
 int64_t fenv_partial_count(const fenv_t *e) { return e ? fenvk::rollout_group_count(e->c) : -1; }
 
 const char *fenv_rollout_kernel(const fenv_t *e, int32_t T) {

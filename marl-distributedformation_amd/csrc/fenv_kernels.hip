@@ -230,7 +230,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
             xpf = xlat_touch<D>(rsg, A, T, act, obs, rew, done);
         float rw;
         bool dn, rs;
-        env_step<MODE, X, !kObsR>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        env_step<MODE, X, !kObsR>(c, p, x, f, a, i, active, ac, s, rw, dn, rs);
         any_reset |= rs;
         const int64_t row = (int64_t)k * A + a;
         if constexpr (OB) {  // obs non-NULL and 16-B aligned (the launcher checks)

@@ -155,7 +155,7 @@ __device__ __forceinline__ void policy_rollout_unit(const Consts &c, const DevSt
         // env.step(clipped actions) (collect_rollouts clips to the Box, vectorized_env.py:68-82)
         float rw;
         bool dn, rs;
-        env_step<MODE>(c, p, x, f, a, i, ac, s, rw, dn, rs);
+        env_step<MODE>(c, p, x, f, a, i, active, ac, s, rw, dn, rs);
         any_reset |= rs;
         if (active) {  // active <=> ln < M; agent a = a_first + ln
             (b.reward + o1)[ln] = rw;

@@ -56,7 +56,7 @@ class ShardedUpdate:
     ``ppo_apply``, include/fenv.h); otherwise torch autograd + ``opt`` (any device)."""
 
     def __init__(self, cfg, obs_dim: int, n_local: list[int], seed: int, device,
-                 fused: bool = False):
+                 fused: bool = False, gen: torch.Generator | None = None):
         self.cfg = cfg
         self.D = int(obs_dim)
         self.world, self.rank = pdist.world_rank()
@@ -66,14 +66,17 @@ class ShardedUpdate:
         self.b, self.M, self.rows, self.bg = minibatch_plan(self.n_local, int(cfg.batch_size),
                                                             self.world)
         self.device = torch.device(device)
-        # each rank shuffles its own samples: a generator per (seed, rank)
-        self.gen = torch.Generator(device=self.device).manual_seed(
+        # each rank shuffles its own samples: a generator per (seed, rank).  `gen` (one rank):
+        # the caller's generator -- ppo.PPO passes the one its replicated path draws SB3's
+        # per-epoch randperm from, so at world 1 both modes run the same minibatches
+        self.gen = gen if gen is not None else torch.Generator(device=self.device).manual_seed(
             (int(seed) * 1_000_003 + self.rank) & 0x7FFFFFFFFFFFFFFF)
         self.fused = bool(fused)
         self.sums = torch.zeros(4, dtype=torch.float64, device=self.device)
 
     # ------------------------------------------------------------------ per update
     def permutations(self) -> torch.Tensor:
+        """[n_epochs, n_local] int64: one randperm per epoch (ppo.epoch_permutations' draws)."""
         n = self.n_local[self.rank]
         perm = torch.empty((self.cfg.n_epochs, n), dtype=torch.long, device=self.device)
         for e in range(self.cfg.n_epochs):

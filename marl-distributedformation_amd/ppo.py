@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes
 import gc
 import math
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -161,8 +162,17 @@ class PPO:
         from . import _lib
         self._ws = (torch.zeros(int(_lib.lib().ppo_workspace_bytes()), dtype=torch.uint8,
                                 device=dev) if self.param.device.type == "cuda" else None)
-        self._dp = (ShardedUpdate(self.cfg, D, [T * c for c in self.counts], seed, dev,
-                                  fused=self.use_fused) if self.sharded else None)
+        self._dp = None
+        if self.sharded:
+            # one rank: the replicated path's generator, so both modes draw the same minibatches
+            self._dp = ShardedUpdate(self.cfg, D, [T * c for c in self.counts], seed, dev,
+                                     fused=self.use_fused,
+                                     gen=self.gen if self.world == 1 else None)
+            if self.world > 1:
+                warnings.warn("PPOConfig(update_mode='sharded'): each rank shuffles its own "
+                              "samples, so the minibatch sequence (and the training trajectory) "
+                              "is not SB3's; update_mode='replicated' reproduces SB3's update "
+                              "exactly", RuntimeWarning, stacklevel=2)
 
     @property
     def num_timesteps(self) -> int:

@@ -271,3 +271,21 @@ def test_sharded_minibatch_plan(pkg):
     assert (b, M, bg[-1]) == (64, 782, 16)  # the reference's 1000 x 5 x 10 samples
     with pytest.raises(ValueError):
         dpu.minibatch_plan([10, 10], 63, 2)
+
+
+def test_sharded_mode_at_world1_draws_sb3_minibatches(pkg):
+    """with one rank, update_mode='sharded' shuffles with the generator the replicated
+    path draws SB3's per-epoch randperm from, so both modes run the same minibatches, over two
+    consecutive updates (the generator advances alike)."""
+    from importlib import import_module
+    dpu = import_module(pkg.__name__ + ".dp_update")
+    ppo = import_module(pkg.__name__ + ".ppo")
+    cfg = ppo.PPOConfig(n_epochs=3)
+    g_rep = torch.Generator().manual_seed(7)
+    g_sh = torch.Generator().manual_seed(7)
+    upd = dpu.ShardedUpdate(cfg, 8, [1000], 7, "cpu", gen=g_sh)
+    for _ in range(2):
+        want = ppo.epoch_permutations(1000, 3, g_rep, "cpu")
+        assert torch.equal(upd.permutations(), want)
+    # the minibatches: contiguous slices of each epoch's permutation, 64 rows, the last 40
+    assert (upd.b, upd.M, upd.bg[-1]) == (64, 16, 40)

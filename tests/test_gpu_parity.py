@@ -695,3 +695,43 @@ def test_philox_reset_draws_match_restatement(venv):
         for ep in (3, 4):
             env.rollout(torch.zeros((4, F * N, 2), device=DEV))
             check(ep, f"auto-reset {ep}")
+
+
+@pytest.mark.parametrize("F,N,mode", [(24, 5, "mt19937"), (24, 5, "philox"), (24581, 5, "mt19937"),
+                                      (3, 100, "mt19937"), (50, 64, "philox")])
+def test_idle_lanes_store_no_terminal_state(venv, flib, F, N, mode):
+    """Root cause of VERDICT r3 weak #1.  Lanes that own no agent -- a wave's lanes
+    past its last whole formation (60-63 at N = 5), the grid's padding waves, a workgroup's
+    threads past N -- run every step from a zero state whose steps_since_reset starts at 0 each
+    launch.  Their phantom done step used to store a zero terminal record at their (f, a) index:
+    another formation's agents, or past the end of the terminal buffer, where the allocator may
+    have put the staged MT19937 reset set (zeroed draws -> wrong post-reset states).  Here the real
+    episodes end one step BEFORE the phantom ones (steps_since_reset 1 at launch start), so a
+    phantom store would overwrite real terminal records: every record must be the real
+    pre-reset, post-clip state of the done step."""
+    import ctypes
+    env = make_env(venv, F, N, True, 12, max_steps=2, reset_mode=mode)
+    env.reset_tensor()
+    px, py, gx, gy, t = env.get_state()
+    env.set_state(px, py, gx, gy, torch.ones_like(t))
+    st0 = [v.cpu().numpy() for v in (px, py, gx, gy)] + [np.ones(F, np.int32)]
+    A = F * N
+    acts = np.stack([synth_actions(77, k, A, 1.2) for k in range(4)])
+    _, _, done = env.rollout(torch.from_numpy(acts).to(DEV))
+    d = done.cpu().numpy()
+    assert d[2].all() and not d[[0, 1, 3]].any()  # real done: step 2; phantom: step 3
+    ref = COracleEnv(F, N, True, 0, max_steps=2)
+    ref.set_state(*st0)
+    ref.step(acts[0])
+    ref.step(acts[1])
+    qx, qy, qgx, qgy, _ = ref.get_state()
+    ex = np.clip(qx + np.float32(10) * acts[2][:, 0], np.float32(0), np.float32(400))
+    ey = np.clip(qy + np.float32(10) * acts[2][:, 1], np.float32(0), np.float32(600))
+    term = np.zeros((A, 4), np.float32)
+    info = (ctypes.c_int64 * 10)()
+    flib.check(flib.lib().fenv_debug_staging(env._h, 4, term.ctypes.data_as(ctypes.c_void_p),
+                                             info), "fenv_debug_staging")
+    want = np.stack([ex, ey, np.repeat(qgx, N), np.repeat(qgy, N)], 1).astype(np.float32)
+    bad = np.nonzero((term.view(np.uint32) != want.view(np.uint32)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} terminal records overwritten, first agents {bad[:8]}"
+    env.check()
