@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede loading libfenv.so: shared HIP runtime
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfenv.so")
 # developer override for A/B builds of the same sources (never needed in normal use)
-LIB_PATH = os.environ.get("FENV_LIB_OVERRIDE", LIB_PATH)
+LIB_PATH = os.environ.get("FENV_LIB_OVERRIDE") or LIB_PATH
 HEADER = os.path.join(os.path.dirname(HERE), "include", "fenv.h")
 
 FENV_RESET_MT19937 = 0

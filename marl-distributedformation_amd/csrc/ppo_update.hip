@@ -40,6 +40,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <type_traits>
@@ -105,7 +108,31 @@ struct PPOArgs {
     // test hook (fenv_test_ppo_inject): the critic block never posts its partial and the actor's
     // wait budget is short, so the launch ends as a lost exchange does
     int32_t inject_lost;
+    // Adam's moment rates as torch uses them: fp32 of (1 - beta) formed in double from the
+    // Python float beta (torch/optim/adam.py: lerp_(grad, 1 - beta1), addcmul_(.., value=1 -
+    // beta2)), not 1 - fp32(beta): for beta2 = 0.999 the two differ by 1.3e-5 relative, a
+    // coherent bias of every second moment (adam_rates below)
+    float omb1, omb2;
 };
+
+// fp32 of (1 - b) for the double b whose shortest decimal form rounds to the fp32 beta (0.9,
+// 0.999: what a Python float beta becomes in ppo_hparams), as torch computes the rate in double.
+static float adam_rate(float beta) {
+    char buf[32];
+    double d = (double)beta;
+    for (int prec = 1; prec <= 9; ++prec) {
+        snprintf(buf, sizeof buf, "%.*g", prec, (double)beta);
+        if (strtof(buf, nullptr) == beta) {
+            d = strtod(buf, nullptr);
+            break;
+        }
+    }
+    return (float)(1.0 - d);
+}
+static void adam_rates(const ppo_hparams &hp, float &omb1, float &omb2) {
+    omb1 = adam_rate(hp.beta1);
+    omb2 = adam_rate(hp.beta2);
+}
 
 // Split launch (FENV_PPO_SPLIT): the actor and the critic each on their own CU.  The two networks'
 // forward, loss and backward are independent; the only coupling is clip_grad_norm_'s global norm,
@@ -139,8 +166,9 @@ __device__ __forceinline__ float tanh_u(float x) {
 #define FENV_PPO_TANH_PK 1
 #endif
 // (An accurate small-argument tanh -- an odd polynomial below |x| = 0.55, where the exp form
-// loses up to 1.4e-3 relative, 1.6e-7 absolute -- was measured 0.5-0.6 us per minibatch slower
-// and no closer to torch; profiles/ab/r3_ppo_tanh_ab.txt, source at commit 2c54623.)
+// loses up to 1.4e-3 relative, 1.6e-7 absolute -- costs 0.5 us per minibatch and lands no closer to
+// torch at the reference config, measured in rounds 3 and 4: profiles/ab/r3_ppo_tanh_ab.txt,
+// profiles/ab/r4_ppo_precision_ab.txt; source at commit 2c54623.)
 __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
 #if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK
     using f2 = float __attribute__((ext_vector_type(2)));
@@ -263,6 +291,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     const PLayout L(D);
     const int P = L.total;
     const ppo_hparams hp = g.hp;
+    const float ar1 = g.omb1, ar2 = g.omb2;  // Adam's (1 - beta) rates (PPOArgs)
     // parameter of Adam slot q of this thread (P: none).  Split: the block's network only --
     // actor = pi* layers, action head, log_std; critic = vf* layers, value head.
     auto own = [&](int q) -> int {
@@ -295,6 +324,15 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         v[q] = (!GRAD && p < P) ? g.exp_avg_sq[p] : 0.0f;
     }
     float step = GRAD ? 0.0f : g.step[0];
+    // beta^step for the bias corrections, carried in double and multiplied by beta per minibatch
+    // (one double pow per launch): (float) of it is the correctly rounded fp32 power torch's
+    // _foreach_pow gives -- exp2f(step * log2f(beta)) was up to 1 ulp off, up to 6e-5 relative in
+    // 1 - beta2^step at the first steps -- and a double pow per minibatch costs ~1.2 us
+    double pw1 = 1.0, pw2 = 1.0;
+    if (!GRAD) {
+        pw1 = pow((double)hp.beta1, (double)step);
+        pw2 = pow((double)hp.beta2, (double)step);
+    }
     // split: the LDS index of each Adam slot's parameter, fixed for the launch; a slot without a
     // parameter points at the pad float after parameter 63 (lx leaves one after every 64; no
     // read ever uses it), so the Adam loop runs branch-free
@@ -308,7 +346,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         }
     }
     bool partner_lost = false;  // split launch: the other block's norm exchange timed out
-    const float lb1 = log2f(hp.beta1), lb2 = log2f(hp.beta2);
     double st_pl = 0.0, st_vl = 0.0, st_el = 0.0, st_cf = 0.0;
 #if FENV_PPO_PROFILE
     double prof[11] = {};
@@ -487,14 +524,14 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             const int ix = SPLIT ? lp[q] : lx(p);
             const float gr = (SPLIT ? gq[q] : G[ix]) * a_coef;
 #if FENV_PPO_ADAM_FMA
-            m[q] = __builtin_fmaf(1.0f - hp.beta1, gr - m[q], m[q]);
-            v[q] = __builtin_fmaf(1.0f - hp.beta2, gr * gr, v[q] * hp.beta2);
+            m[q] = __builtin_fmaf(ar1, gr - m[q], m[q]);
+            v[q] = __builtin_fmaf(ar2, gr * gr, v[q] * hp.beta2);
             const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v[q]), a_ib, hp.eps);
             const float wn = __builtin_fmaf(-a_ss, m[q] * __builtin_amdgcn_rcpf(den),
                                             SPLIT ? wq[q] : W[ix]);
 #else
-            m[q] = m[q] + (1.0f - hp.beta1) * (gr - m[q]);
-            v[q] = v[q] * hp.beta2 + (1.0f - hp.beta2) * (gr * gr);
+            m[q] = m[q] + ar1 * (gr - m[q]);
+            v[q] = v[q] * hp.beta2 + ar2 * (gr * gr);
             // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
             // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
             const float den = __builtin_amdgcn_sqrtf(v[q]) * a_ib + hp.eps;
@@ -511,7 +548,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         const f2 g = {gq[q], gq[q + 1]};
         const f2 gr = g * a_coef;
         f2 mm = {m[q], m[q + 1]}, vv = {v[q], v[q + 1]};
-        const f2 c1 = 1.0f - hp.beta1, c2 = 1.0f - hp.beta2;
+        const f2 c1 = ar1, c2 = ar2;
         mm = __builtin_elementwise_fma(c1, gr - mm, mm);
         vv = __builtin_elementwise_fma(c2, gr * gr, vv * hp.beta2);
         const f2 sq = {__builtin_amdgcn_sqrtf(vv.x), __builtin_amdgcn_sqrtf(vv.y)};
@@ -863,9 +900,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 // kBCW: this minibatch's Adam bias corrections (they depend on the step count
                 // only), by a wave that would otherwise wait out the loss at the barrier; every
                 // thread reads them after the norm exchange instead of computing them there
-                const float sn = step + 1.0f;
-                const float bc1 = 1.0f - exp2f(sn * lb1);  // 1 - beta1^step
-                const float bc2 = 1.0f - exp2f(sn * lb2);
+                pw1 *= (double)hp.beta1;  // beta^(step + 1)
+                pw2 *= (double)hp.beta2;
+                const float bc1 = 1.0f - (float)pw1;
+                const float bc2 = 1.0f - (float)pw2;
                 const float ss = hp.lr / bc1, ib = 1.0f / __builtin_sqrtf(bc2);
                 if (lane == 0) {
                     R[kBC] = ss;
@@ -1298,8 +1336,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 a_ib = R[kBC + 1];
             } else {
                 step += 1.0f;
-                const float bc1 = 1.0f - exp2f(step * lb1);  // 1 - beta1^step
-                const float bc2 = 1.0f - exp2f(step * lb2);
+                pw1 *= (double)hp.beta1;
+                pw2 *= (double)hp.beta2;
+                const float bc1 = 1.0f - (float)pw1;
+                const float bc2 = 1.0f - (float)pw2;
                 a_ss = hp.lr / bc1;
                 a_ib = 1.0f / __builtin_sqrtf(bc2);
             }
@@ -1362,9 +1402,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 constexpr int kAT = 1024;
 __global__ __launch_bounds__(kAT) void k_ppo_apply(float *params, float *exp_avg,
                                                    float *exp_avg_sq, float *step,
-                                                   const float *grad, int P, ppo_hparams hp) {
+                                                   const float *grad, int P, ppo_hparams hp,
+                                                   float omb1, float omb2) {
     __shared__ float red[kAT / 64];
-    __shared__ float s_coef, s_step;
+    __shared__ float s_coef, s_step, s_bc1, s_bc2;
     const int tid = threadIdx.x;
     float ss = 0.f;
     for (int p = tid; p < P; p += kAT) ss = __builtin_fmaf(grad[p], grad[p], ss);
@@ -1379,16 +1420,19 @@ __global__ __launch_bounds__(kAT) void k_ppo_apply(float *params, float *exp_avg
         s_coef = c < 1.0f ? c : 1.0f;
         s_step = step[0] + 1.0f;
         step[0] = s_step;
+        // 1 - beta^step, beta^step the correctly rounded fp32 power (torch's _foreach_pow)
+        s_bc1 = 1.0f - (float)pow((double)hp.beta1, (double)s_step);
+        s_bc2 = 1.0f - (float)pow((double)hp.beta2, (double)s_step);
     }
     __syncthreads();
-    const float coef = s_coef, st = s_step;
-    const float bc1 = 1.0f - powf(hp.beta1, st), bc2 = 1.0f - powf(hp.beta2, st);
+    const float coef = s_coef;
+    const float bc1 = s_bc1, bc2 = s_bc2;
     const float step_size = hp.lr / bc1, ssn = -step_size;
     const float bc2s = __builtin_sqrtf(bc2);
     for (int p = tid; p < P; p += kAT) {
         const float gr = grad[p] * coef;
-        const float m = exp_avg[p] + (1.0f - hp.beta1) * (gr - exp_avg[p]);  // lerp_, weight < 0.5
-        const float v = exp_avg_sq[p] * hp.beta2 + (1.0f - hp.beta2) * gr * gr;  // mul_ + addcmul_
+        const float m = exp_avg[p] + omb1 * (gr - exp_avg[p]);  // lerp_, weight < 0.5
+        const float v = exp_avg_sq[p] * hp.beta2 + omb2 * gr * gr;  // mul_ + addcmul_
         exp_avg[p] = m;
         exp_avg_sq[p] = v;
         const float denom = __builtin_sqrtf(v) / (bc2s * ssn) + hp.eps / ssn;
@@ -1456,9 +1500,21 @@ hipError_t launch_ppo_update(float *params, float *exp_avg, float *exp_avg_sq, f
     PPOArgs g{params, exp_avg, exp_avg_sq, step, obs, act, old_log_prob, adv, ret, perm, n,
               D, n_epochs, batch_size, hp, stats, xch, nullptr, 0.f, 0.f, 1.f, 0, 1,
               split ? ppo_take_inject() : 0};
-    if (split)
-        hipLaunchKernelGGL(k_ppo_update<true>, dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
-    else
+    adam_rates(hp, g.omb1, g.omb2);
+    if (split) {
+        // A cooperative launch: the runtime admits the grid only when all 9 workgroups are
+        // resident at once, so the actor and critic blocks cannot wait for a partner that is
+        // queued behind other work (the bounded spin remains as a guard, and the inject hook
+        // still exercises it).  Blocks 0 and 8 work; the dispatcher's round-robin puts them on
+        // one XCD, so their exchange words stay in that XCD's L2.
+        void *args[] = {&g};
+        e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&k_ppo_update<true>),
+                                       dim3(9), dim3(kPTS), args, (unsigned)kPPOLdsBytes, st);
+        if (e != hipSuccess) {
+            if (own_ws) (void)hipFreeAsync(xch, st);
+            return e;
+        }
+    } else
         hipLaunchKernelGGL(k_ppo_update<false>, dim3(1), dim3(kPT), kPPOLdsBytes, st, g);
     e = hipGetLastError();
     if (own_ws) {
@@ -1481,6 +1537,7 @@ hipError_t launch_ppo_grad(const float *params, int32_t D, const float *obs, con
               adv, ret, rows, (int64_t)b_local, D, 1, b_local, hp, stats, nullptr, grad,
               1.0f / (float)b_global, adv_mean, adv_std,
               (adv_normalize && b_global > 1) ? 1 : 0, entropy_term ? 1 : 0, 0};
+    adam_rates(hp, g.omb1, g.omb2);
     hipLaunchKernelGGL((k_ppo_update<true, true>), dim3(9), dim3(kPTS), kPPOLdsBytes, st, g);
     return hipGetLastError();
 }
@@ -1489,8 +1546,10 @@ hipError_t launch_ppo_apply(float *params, float *exp_avg, float *exp_avg_sq, fl
                             const float *grad, int32_t D, const ppo_hparams &hp,
                             hipStream_t st) {
     const PLayout L(D);
+    float omb1, omb2;
+    adam_rates(hp, omb1, omb2);
     hipLaunchKernelGGL(k_ppo_apply, dim3(1), dim3(kAT), 0, st, params, exp_avg, exp_avg_sq, step,
-                       grad, L.total, hp);
+                       grad, L.total, hp, omb1, omb2);
     return hipGetLastError();
 }
 
