@@ -7,7 +7,8 @@ agents (5,242,880 agents).  Formations are independent, so the ranks own disjoin
 formation shards of one global env with no data-path collective.  With N > 1 GPUs the headline
 is config 3 as written -- the 1M formations split over the ranks (strong scaling, `"scaling":
 "strong"`) -- and the same line nests the weak-scaling measurement (1M formations on every rank,
-`weak_scaling_line`); `--scaling weak` swaps the two, `--no-weak-line` skips the nested one.  A "step" is one env step of every agent; steps run as fused rollouts of
+`weak_scaling_line`); `--scaling weak` swaps the two, `--no-weak-line` skips the nested one.
+A "step" is one env step of every agent; steps run as fused rollouts of
 `--chunk` steps per launch (SB3's n_steps=10 rollout, vectorized_env.py:128) writing obs /
 reward / done for every step into a device rollout buffer, with the actions read from HBM
 (inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
@@ -201,12 +202,15 @@ SIMDS, SCLK_HZ = 1024, 2.4e9  # MI355X: 256 CUs x 4 SIMDs, 2.4 GHz peak engine c
 def policy_rollout_roofline(kernel_ms: float):
     """Roofline of the fused policy rollout (k_policy_rollout): it is bound by VALU issue, not by
     HBM (~78 B per agent-step) or the MFMA pipe.  achieved = the kernel's VALU-active SIMD-cycles
-    per launch (SQ_ACTIVE_INST_VALU x 4, PMC, profiles/r2_policy_pmc_sq.json) / the launch time
+    per launch (SQ_ACTIVE_INST_VALU x 4, PMC, profiles/r4_policy_pmc_sq.json) / the launch time
     measured live in this run; peak = every SIMD's VALU busy every cycle (1024 x 2.4 GHz).
     mfma_busy_frac the same way from SQ_VALU_MFMA_BUSY_CYCLES."""
-    p = os.path.join(ROOT, "profiles", "r2_policy_pmc_sq.json")
-    if not os.path.exists(p):
+    # the PMC passes of the current round (tools/policy_pmc.sh at HEAD), else an older round's
+    src = next((f for f in ("r4_policy_pmc_sq.json", "r2_policy_pmc_sq.json")
+                if os.path.exists(os.path.join(ROOT, "profiles", f))), None)
+    if src is None:
         return None
+    p = os.path.join(ROOT, "profiles", src)
     ks = json.load(open(p)).get("kernels", {})
     k = next((v for n, v in ks.items() if "k_policy_rollout" in n), None)
     if not k or "SQ_ACTIVE_INST_VALU" not in k:
@@ -217,7 +221,7 @@ def policy_rollout_roofline(kernel_ms: float):
            "unit": "VALU-active SIMD-cycles/s", "frac": valu / peak,
            "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
            "kernel": "k_policy_rollout (fenv_policy_rollout)", "kernel_ms": kernel_ms,
-           "pmc_source": "profiles/r2_policy_pmc_sq.json"}
+           "pmc_source": f"profiles/{src}"}
     if "SQ_VALU_MFMA_BUSY_CYCLES" in k:
         out["mfma_busy_frac"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (kernel_ms * 1e-3) / peak
     if "SQ_WAVE_CYCLES" in k:
