@@ -23,10 +23,6 @@ if [ -z "${SKIP_DEFAULT:-}" ]; then
   echo "bench(default) done"
 fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_driver" -o bench \
-  -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver_under_rocprof.json" 2> "$O/prof_driver.err" \
-  || fatal $? rocprof
-echo "rocprof ok"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$R/gpurun_out/pmc_${TAG}_$C" -o pmc \
     -- python3 "$R/bench.py" --steps 200 --warmup 20 --prewarm-ms 50 --no-cpu-baseline --no-stats --no-policy --no-configs \
@@ -34,3 +30,10 @@ for C in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $C ok"
 done
 python3 "$R/tools/pmc_summary.py" "$R/gpurun_out" "$TAG" > "$O/pmc_summary.txt" 2>&1; echo "pmc summary rc=$?"
+# Last: rocprofv3 (ROCm 7.2) segfaults inside exit(), after its output is written, when the
+# profiled process made a cooperative launch (the PPO update's split launch; DESIGN §8 round 4,
+# profiles/r4_rocprof_coop_exit/), so nothing may follow it in this call.
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_driver" -o bench \
+  -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver_under_rocprof.json" 2> "$O/prof_driver.err" \
+  || fatal $? rocprof
+echo "rocprof ok"
