@@ -14,10 +14,13 @@ this module writes and reads the SB3 2.x ``save_to_zip_file`` layout itself:
 
 Loading reads ``policy.pth`` with ``torch.load(weights_only=True)`` only (no pickle
 execution), so zips written by real SB3 load here too.  Zips written here carry the same entry
-names and tensors; SB3's ``data`` entries for ``policy_class``, ``observation_space`` and
-``action_space`` are cloudpickled gymnasium/SB3 objects that cannot be produced without those
-packages, so an SB3 ``PPO.load`` of them needs ``custom_objects`` for those three keys
-(INTEGRATION.md).  Parity against SB3 itself: unpinned (SB3 absent).
+names and tensors.  SB3's ``data`` entries for ``policy_class``, ``observation_space`` and
+``action_space`` are cloudpickled SB3 / gymnasium objects; round 4 writes them as the pickles
+cloudpickle would (``sb3_pickle.py``: the policy class by reference, the reference's two
+``Box`` spaces), so the reference's own playback, ``PPO.load(checkpoint_path)`` with no
+``custom_objects`` (visualize_policy.py:35), has what it needs.  The Adam state's param group
+is written with SB3's optimizer settings (non-capturable Adam), so ``set_parameters`` loads it
+on any device.  Parity against SB3 itself: unpinned (SB3 and gymnasium absent).
 """
 from __future__ import annotations
 
@@ -28,6 +31,8 @@ import platform
 import zipfile
 
 import torch
+
+from . import sb3_pickle
 
 SB3_VERSION = "2.3.2"  # the version string written into _stable_baselines3_version
 
@@ -43,10 +48,10 @@ SB3_PARAM_ORDER = [
     "value_net.weight", "value_net.bias",
 ]
 
-# keys of SB3's saved ``data`` whose values are pickled objects (need custom_objects in SB3)
-_OPAQUE = {"policy_class": "<class 'stable_baselines3.common.policies.ActorCriticPolicy'>",
-           "observation_space": "<class 'gymnasium.spaces.box.Box'>",
-           "action_space": "<class 'gymnasium.spaces.box.Box'>"}
+# the param-group settings of the Adam SB3's ActorCriticPolicy builds (torch defaults, eps 1e-5
+# set by the policy): a saved group carries them so that SB3 loads it as its own
+_SB3_ADAM_GROUP = {"weight_decay": 0, "amsgrad": False, "maximize": False, "foreach": None,
+                   "capturable": False, "differentiable": False, "fused": None}
 
 
 def _tensor_bytes(obj) -> bytes:
@@ -80,6 +85,7 @@ def optimizer_state_from_flat(shapes: list[tuple[str, tuple]], opt_state: dict) 
                     "exp_avg": st["exp_avg"][a:a + n].detach().cpu().reshape(shp).clone(),
                     "exp_avg_sq": st["exp_avg_sq"][a:a + n].detach().cpu().reshape(shp).clone()}
     g = {k: v for k, v in groups[0].items() if k != "params"}
+    g.update(_SB3_ADAM_GROUP)
     g["params"] = list(range(len(SB3_PARAM_ORDER)))
     return {"state": state, "param_groups": [g]}
 
@@ -155,8 +161,11 @@ def save_sb3_zip(path: str, state_dict: dict, *, num_timesteps: int, data: dict 
     missing = [k for k in SB3_PARAM_ORDER if k not in state_dict]
     if missing:
         raise KeyError(f"state_dict lacks SB3 parameters {missing}")
-    d = {k: {":type:": t, ":serialized:": ""} for k, t in _OPAQUE.items()}
-    d.update({"num_timesteps": int(num_timesteps), "_total_timesteps": int(num_timesteps)})
+    obs_dim = int(state_dict["mlp_extractor.policy_net.0.weight"].shape[1])
+    act_dim = int(state_dict["action_net.weight"].shape[0])
+    d = sb3_pickle.sb3_opaque_entries(obs_dim, act_dim)
+    d.update({"num_timesteps": int(num_timesteps), "_total_timesteps": int(num_timesteps),
+              "policy_kwargs": {}})
     d.update(data or {})
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     # the partial file's name must not look like a checkpoint to latest_checkpoint's rule

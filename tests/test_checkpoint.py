@@ -48,6 +48,91 @@ def test_zip_roundtrip_and_layout(ck, shapes, tmp_path):
         assert torch.equal(sd3[k], sd[k])
 
 
+def _standin_modules(monkeypatch):
+    """Stand-ins for the two classes the pickled entries name, restating what unpickling uses
+    of them: gymnasium's Space.__setstate__ / Box.__setstate__ (legacy-key handling, then a
+    __dict__ update; low_repr / high_repr re-derived when absent) and SB3's policy class."""
+    import sys
+    import types
+
+    class Box:
+        @property
+        def shape(self):
+            return self._shape
+
+        def __setstate__(self, state):
+            state = dict(state)
+            if "shape" in state:
+                state["_shape"] = state.pop("shape")
+            if "np_random" in state:
+                state["_np_random"] = state.pop("np_random")
+            self.__dict__.update(state)
+
+    class ActorCriticPolicy:
+        pass
+
+    mods = {}
+    for name in ("gymnasium", "gymnasium.spaces", "gymnasium.spaces.box", "stable_baselines3",
+                 "stable_baselines3.common", "stable_baselines3.common.policies"):
+        mods[name] = types.ModuleType(name)
+        monkeypatch.setitem(sys.modules, name, mods[name])
+    Box.__module__, ActorCriticPolicy.__module__ = "gymnasium.spaces.box", \
+        "stable_baselines3.common.policies"
+    mods["gymnasium.spaces.box"].Box = Box
+    mods["stable_baselines3.common.policies"].ActorCriticPolicy = ActorCriticPolicy
+    return Box, ActorCriticPolicy
+
+
+def test_pickled_entries_load_as_sb3_does(ck, shapes, tmp_path, monkeypatch):
+    """What SB3's PPO.load (save_util.json_to_data: base64 -> cloudpickle.loads) gets from the
+    three pickled ``data`` entries, which the reference's playback needs with no custom_objects
+    (visualize_policy.py:35): the policy class and the reference's two Box spaces
+    (vectorized_env.py:34-35).  Parity against SB3 / gymnasium themselves: unpinned."""
+    import base64
+    import pickle
+    import warnings
+
+    import numpy as np
+    Box, ACP = _standin_modules(monkeypatch)
+    p = ck.save_sb3_zip(str(tmp_path / "m"), random_sd(shapes), num_timesteps=7)
+    with zipfile.ZipFile(p) as z:
+        data = json.loads(z.read("data"))
+    assert data["policy_class"][":type:"] == "<class 'abc.ABCMeta'>"
+    assert data["observation_space"][":type:"] == "<class 'gymnasium.spaces.box.Box'>"
+    assert data["policy_kwargs"] == {}
+    out = {}
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # numpy.core names must load without a deprecation
+        for k in ("policy_class", "observation_space", "action_space"):
+            out[k] = pickle.loads(base64.b64decode(data[k][":serialized:"].encode()))
+    assert out["policy_class"] is ACP
+    for k, dim in (("observation_space", 8), ("action_space", 2)):
+        b = out[k]
+        assert type(b) is Box and b.shape == (dim,) and b.dtype == np.float32
+        assert b.low.dtype == np.float32 and b.high.dtype == np.float32
+        assert np.array_equal(b.low, np.full(dim, -1, np.float32))
+        assert np.array_equal(b.high, np.full(dim, 1, np.float32))
+        assert b.bounded_below.dtype == np.bool_ and b.bounded_below.all()
+        assert b.bounded_above.all() and b.low_repr == "-1.0" and b.high_repr == "1.0"
+        assert b._np_random is None and b.low.flags.writeable
+
+
+def test_optimizer_group_is_sb3s(ck, shapes):
+    """The saved Adam param group carries SB3's optimizer settings (a non-capturable Adam), so
+    SB3's set_parameters loads it on any device; lr / betas / eps are the trained ones."""
+    n = sum(int(torch.tensor(s).prod()) for _, s in shapes)
+    p = torch.nn.Parameter(torch.zeros(n))
+    opt = torch.optim.Adam([p], lr=1e-3, eps=1e-5, capturable=False)
+    p.grad = torch.ones(n)
+    opt.step()
+    sd = opt.state_dict()
+    sd["param_groups"][0]["capturable"] = True
+    g = ck.optimizer_state_from_flat(shapes, sd)["param_groups"][0]
+    assert g["capturable"] is False and g["foreach"] is None and g["fused"] is None
+    assert g["lr"] == 1e-3 and g["eps"] == 1e-5 and tuple(g["betas"]) == (0.9, 0.999)
+    assert g["params"] == list(range(13))
+
+
 def test_zip_rejects_incomplete_state(ck, shapes, tmp_path):
     sd = random_sd(shapes)
     del sd["log_std"]
