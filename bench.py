@@ -325,6 +325,34 @@ def random_action_bench(pkgname: str, dev, formations: int, agents: int, launche
             "hbm_gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def numpy_face_bench(pkgname: str, dev, formations: int, agents: int, steps: int) -> dict:
+    """The PCIe-inclusive rate: the reference's own interface, ``FormationEnv.step(np.ndarray)``
+    (vectorized_env.py:68-82, what SB3's VecEnv loop calls), which copies the actions host ->
+    device and obs / reward / done device -> host through pinned buffers every step.  Never the
+    headline `value` (its inputs are not HBM-resident)."""
+    import numpy as np
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode="philox")
+    A = env.num_envs
+    rng = np.random.default_rng(7)
+    acts = [rng.uniform(-1, 1, (A, 2)).astype(np.float32) for _ in range(2)]
+    env.reset()
+    for k in range(3):
+        env.step(acts[k % 2])
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(acts[k % 2])
+    el = time.perf_counter() - t0
+    env.release()
+    pcie_b = A * (2 * 4 + 8 * 4 + 4 + 1)  # actions in; obs, reward, done out
+    return {"workload": f"{formations} formations x {agents} agents, FormationEnv.step(numpy) "
+                        f"x {steps}", "value": A * steps / el, "unit": "agent-steps/s",
+            "ms_per_step": 1e3 * el / steps, "pcie_bytes_per_step": pcie_b,
+            "pcie_gbs": pcie_b * steps / el / 1e9}
+
+
 def secondary(fn, *a):
     """A secondary line (after the timed region): an error in it is reported in its own field
     instead of taking the headline line down with it."""
@@ -766,6 +794,11 @@ def main():
         if world == 1 and not args.no_policy:
             out["ppo_update"] = secondary(ppo_update_bench, pkg.__name__, dev)
         if world == 1 and not args.no_configs:
+            # the PCIe-inclusive numpy face: the reference's default size (config 0) and the
+            # headline size
+            out["numpy_face"] = {
+                "config0": secondary(numpy_face_bench, pkg.__name__, dev, 1000, N, 200),
+                "config3": secondary(numpy_face_bench, pkg.__name__, dev, args.formations, N, 10)}
             out["random_action_rollout"] = random_action_bench(pkg.__name__, dev,
                                                                args.formations, N)
             out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),

@@ -13,6 +13,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -223,6 +224,15 @@ struct fenv {
     float *lf = nullptr;     // device: large-formation exchange scratch (N > 1024 only)
     std::mt19937 mt;         // the reference's global stream (all formations of all shards)
     int64_t t_common = 0;    // steps_since_reset shared by all formations, -1 if not uniform
+    // The next set is drawn ahead, on a host thread, while the device runs the episode: at a
+    // reset event the host only stages a set drawn ~1,000 steps earlier (a config-3 set is 12.6M
+    // MT19937 draws, tens of ms of host time, about one episode of device time).  The thread
+    // does CPU work only -- mt, the host slot `ahead_slot`, its tags -- never a HIP call, so it
+    // cannot disturb a stream capture elsewhere in the process.  mt and that host slot belong
+    // to the thread until it is joined (join_ahead), and nothing else touches mt.
+    std::thread ahead;
+    int ahead_slot = -1;     // host slot the thread is drawing into (-1: none)
+    uint32_t ahead_gen = 0;  // the generation it is drawing
 
     size_t pend_floats() const { return (size_t)fenvk::stage_floats(A, c.F); }
     size_t pend_stride() const { return (pend_floats() + 63) & ~(size_t)63; }  // 256-B slots
@@ -253,23 +263,15 @@ struct fenv {
         return FENV_OK;
     }
 
-    // Called right after the launch that consumed slot rd was queued on `st`: draw the next
-    // reset set of the global stream, keep this shard's part, stage it into the other slot.
-    int gen_pending(hipStream_t st) {
-        if (c.reset_mode != FENV_RESET_MT19937) return FENV_OK;
-        const int w = rd ^ 1;
-        if (pend_ev_recorded[rd]) {  // slot rd now has a queued reader on st
-            FENV_HIP(hipEventRecord(used_ev[rd], st));
-            used_ev_recorded[rd] = true;
-        }
-        if (pend_ev_recorded[w]) FENV_HIP(hipEventSynchronize(pend_ev[w]));  // host slot free
+    // Draw the global stream's next reset set, keep this shard's part in host slot w with its
+    // tags (generation gen).  CPU only: runs on the calling thread or on `ahead`.
+    void draw_set(int w, uint32_t gen) {
         const size_t off = (size_t)w * pend_stride();
         const uint64_t per = 2ull * (uint64_t)c.N + 2ull;
         mt.discard(per * (uint64_t)c.f0);
         float *hp = hpend + off;
         float *px = hp, *py = hp + A, *gx = hp + 2 * A, *gy = hp + 2 * A + c.F;
         uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F), *gt = at + A;
-        const uint32_t gen = gen_next++;
         for (int64_t f = 0; f < c.F; ++f) {
             draw_formation(mt, c.N, px + f * c.N, py + f * c.N, gx[f], gy[f]);
             for (int64_t a = f * c.N; a < (f + 1) * c.N; ++a) {
@@ -284,6 +286,36 @@ struct fenv {
             gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
         }
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
+    }
+
+    // Wait for the draw-ahead thread (if any); afterwards mt and both host slots are the
+    // caller's again.
+    void join_ahead() {
+        if (ahead.joinable()) ahead.join();
+    }
+
+    // Called right after the launch that consumed slot rd was queued on `st`: stage the global
+    // stream's next reset set into the other slot (drawn ahead, or now if no draw is ahead),
+    // then start drawing the set after it into the host slot just consumed.
+    int gen_pending(hipStream_t st) {
+        if (c.reset_mode != FENV_RESET_MT19937) return FENV_OK;
+        const int w = rd ^ 1;
+        if (pend_ev_recorded[rd]) {  // slot rd now has a queued reader on st
+            FENV_HIP(hipEventRecord(used_ev[rd], st));
+            used_ev_recorded[rd] = true;
+        }
+        uint32_t gen;
+        if (ahead_slot == w) {
+            join_ahead();
+            gen = ahead_gen;
+        } else {
+            join_ahead();
+            if (pend_ev_recorded[w]) FENV_HIP(hipEventSynchronize(pend_ev[w]));  // host slot free
+            gen = gen_next++;
+            draw_set(w, gen);
+        }
+        ahead_slot = -1;
+        const size_t off = (size_t)w * pend_stride();
         // the slot's previous reader (the launch that consumed it, on whatever stream) first
         if (used_ev_recorded[w]) FENV_HIP(hipStreamWaitEvent(st, used_ev[w], 0));
         int32_t mode = 0;
@@ -295,6 +327,17 @@ struct fenv {
         FENV_HIP(hipEventRecord(pend_ev[w], st));
         pend_ev_recorded[w] = true;
         rd = w;
+        // draw ahead into host slot w ^ 1 once its own copy (queued at the previous refill) has
+        // read it: in steady state that copy finished an episode ago
+        const int nx = w ^ 1;
+        if (pend_ev_recorded[nx]) FENV_HIP(hipEventSynchronize(pend_ev[nx]));
+        try {
+            ahead = std::thread([this, nx, g = gen_next]() { draw_set(nx, g); });
+            ahead_slot = nx;
+            ahead_gen = gen_next++;
+        } catch (...) {  // no thread to be had: the next refill draws on the caller's thread
+            ahead_slot = -1;
+        }
         return FENV_OK;
     }
 
@@ -435,6 +478,7 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
 int fenv_destroy(fenv_t *e) {
     if (!e) return FENV_OK;
     if (!live_take(e)) return fail(FENV_EINVAL, "fenv_destroy: not a live handle (destroyed twice?)");
+    e->join_ahead();  // the draw-ahead thread writes the host slots freed below
     // Safe at any point: the caller's current device is restored; the handle's own staging copy
     // is waited for (hipFree then waits for the device's kernels); a free the runtime refuses
     // during a stream capture is parked and retried later instead of failing the capture.
@@ -488,6 +532,7 @@ int64_t fenv_pinned_pool_bytes(int32_t device) { return (int64_t)pinned_cached(d
 
 int fenv_debug_staging(fenv_t *e, int32_t which, float *out_host, int64_t *info_host) {
     if (!e || !info_host) return fail(FENV_EINVAL, "fenv_debug_staging: NULL argument");
+    e->join_ahead();
     info_host[0] = e->rd;
     info_host[1] = e->slot_gen[0];
     info_host[2] = e->slot_gen[1];

@@ -321,3 +321,17 @@ def test_pinned_pool_bounded_under_growing_sizes(venv, flib):
     small.reset()
     small.release()
     assert L.fenv_pinned_pool_bytes(0) <= 512 << 20
+
+
+def test_mt_draw_ahead_across_events_and_release(venv, flib):
+    """The next MT19937 set is drawn ahead on a host thread (fenv_api.cpp gen_pending): at
+    200,000 x 5 (2.4M draws per set) and a reset event every 4 steps, every staged set equals the
+    oracle's, in order, across calls of several lengths and two streams; releasing the env with
+    a draw in flight joins it (the host slots it writes are freed after), and the next env --
+    which may take the same pinned buffer -- is bit-exact again."""
+    env, bad = _mt_run(venv, 200_000, 5, 31, (3, 5, 9, 2, 7))
+    assert bad is None, bad
+    env.release()
+    env, bad = _mt_run(venv, 200_000, 5, 32, (6, 1, 4), streams=True)
+    assert bad is None, bad
+    env.release()
