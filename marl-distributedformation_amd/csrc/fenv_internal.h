@@ -47,13 +47,19 @@ __host__ __device__ inline uint32_t stage_mix(uint32_t x) {
     x *= 0xC2B2AE35u;
     return x ^ (x >> 16);
 }
+__host__ __device__ inline uint32_t stage_rotl13(uint32_t x) { return (x << 13) | (x >> 19); }
+// One finaliser round over the draw's bits, the generation and the index: a bijection of the
+// combined word, so a draw read under another generation (or a stale value) mismatches unless
+// the combination collides (~2^-32 per draw); one round keeps the host's tagging of a config-3
+// set (5.2M agents) off the refill's critical path.
 __host__ __device__ inline uint32_t stage_tag_agent(uint32_t gen, int64_t a, uint32_t bx,
                                                     uint32_t by) {
-    return stage_mix(bx ^ stage_mix(by ^ stage_mix(gen ^ ((uint32_t)a * 0x9E3779B1u))));
+    return stage_mix(bx ^ stage_rotl13(by) ^ (gen * 0x85EBCA6Bu) ^ ((uint32_t)a * 0x9E3779B1u));
 }
 __host__ __device__ inline uint32_t stage_tag_goal(uint32_t gen, int64_t f, uint32_t bx,
                                                    uint32_t by) {
-    return stage_mix(bx ^ stage_mix(by ^ stage_mix(gen ^ 0x5BD1E995u ^ ((uint32_t)f * 0x85EBCA6Bu))));
+    return stage_mix(bx ^ stage_rotl13(by) ^ (gen * 0x85EBCA6Bu) ^ 0x5BD1E995u ^
+                     ((uint32_t)f * 0x9E3779B1u));
 }
 // floats of one staged set (tags are 32-bit words in float slots)
 inline int64_t stage_floats(int64_t A, int64_t F) { return 3 * A + 3 * F; }

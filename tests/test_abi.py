@@ -46,7 +46,10 @@ def test_desired_neighbor_dist(flib, N):
 
 @pytest.mark.parametrize("N,total,first,count,skip", [(5, 7, 0, 7, 0), (5, 7, 2, 3, 1),
                                                       (10, 4, 3, 1, 2), (64, 3, 1, 2, 0),
-                                                      (1, 9, 4, 5, 3)])
+                                                      (1, 9, 4, 5, 3),
+                                                      # discards of many whole 624-word blocks
+                                                      # from every offset in a block
+                                                      (5, 2000, 700, 300, 2), (7, 501, 13, 488, 5)])
 def test_host_reset_draws_match_torch_stream(flib, N, total, first, count, skip):
     """Draw set `skip` of the global stream, restricted to formations [first, first+count),
     equals torch.rand after torch.manual_seed (the reference's RNG, simulate.py:133-143)."""
