@@ -39,34 +39,30 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 // MT19937 (Matsumoto & Nishimura 1998; init_genrand seeding, as torch's CPU generator after
 // torch.manual_seed and as std::mt19937), producing the same sequence as std::mt19937 but
-// twisting and tempering the 624-word state a block at a time in straight loops the compiler
-// vectorises (~2.5x the draws per second of libstdc++'s per-draw branch at -O3 on x86-64), and
-// skipping whole blocks in discard without tempering them.  Pinned bit for bit to the oracle's
+// twisting the 624-word state a block at a time and tempering runs of it straight into the
+// caller's buffer (`fill`), in loops the compiler vectorises, and skipping whole blocks in
+// discard without tempering them: a config-3 set with its tags takes ~1/3 of the host time
+// of libstdc++'s per-draw generator (§9.2).  Pinned bit for bit to the oracle's
 // MT19937 by tests/test_oracle_golden.py (fenv_host_reset_draws) and to the reference's draws
 // by the golden fixtures.
 class Mt19937 {
     static constexpr int kN = 624, kM = 397;
     uint32_t s_[kN];
-    uint32_t out_[kN];
     int pos_ = kN;
     static uint32_t tw(uint32_t a, uint32_t b, uint32_t m) {
         const uint32_t y = (a & 0x80000000u) | (b & 0x7FFFFFFFu);
         return m ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908B0DFu);
     }
+    static uint32_t temper(uint32_t y) {
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9D2C5680u;
+        y ^= (y << 15) & 0xEFC60000u;
+        return y ^ (y >> 18);
+    }
     void twist() {
         for (int i = 0; i < kN - kM; ++i) s_[i] = tw(s_[i], s_[i + 1], s_[i + kM]);
         for (int i = kN - kM; i < kN - 1; ++i) s_[i] = tw(s_[i], s_[i + 1], s_[i + kM - kN]);
         s_[kN - 1] = tw(s_[kN - 1], s_[0], s_[kM - 1]);
-    }
-    void refill() {
-        twist();
-        for (int i = 0; i < kN; ++i) {
-            uint32_t y = s_[i];
-            y ^= y >> 11;
-            y ^= (y << 7) & 0x9D2C5680u;
-            y ^= (y << 15) & 0xEFC60000u;
-            out_[i] = y ^ (y >> 18);
-        }
         pos_ = 0;
     }
 
@@ -78,20 +74,21 @@ class Mt19937 {
             s_[i] = 1812433253u * (s_[i - 1] ^ (s_[i - 1] >> 30)) + (uint32_t)i;
         pos_ = kN;
     }
-    uint32_t operator()() {
-        if (pos_ == kN) refill();
-        return out_[pos_++];
-    }
-    void discard(uint64_t n) {
+    // the next n draws into d[0..n), tempered straight from the state a block at a time
+    void fill(uint32_t *d, size_t n) {
         while (n) {
-            if (pos_ == kN) {
-                if (n >= (uint64_t)kN) {  // a whole block: twist, no tempering
-                    twist();
-                    n -= kN;
-                    continue;
-                }
-                refill();
-            }
+            if (pos_ == kN) twist();
+            const size_t k = std::min<size_t>(n, (size_t)(kN - pos_));
+            const uint32_t *src = s_ + pos_;
+            for (size_t i = 0; i < k; ++i) d[i] = temper(src[i]);
+            d += k;
+            n -= k;
+            pos_ += (int)k;
+        }
+    }
+    void discard(uint64_t n) {  // whole blocks are twisted, never tempered
+        while (n) {
+            if (pos_ == kN) twist();
             const uint64_t k = std::min<uint64_t>(n, (uint64_t)(kN - pos_));
             pos_ += (int)k;
             n -= k;
@@ -102,19 +99,46 @@ class Mt19937 {
 // torch.rand float32 from one 32-bit MT19937 draw.
 inline float u24(uint32_t r) { return (float)(r & 0xFFFFFFu) * 0x1.0p-24f; }
 
-// One formation's reset draws (simulate.py:133-143): N (x, y) pairs then the goal pair.
-inline void draw_formation(Mt19937 &mt, int32_t N, float *px, float *py, float &gx,
-                           float &gy) {
-    for (int32_t j = 0; j < N; ++j) {
-        const float ux = u24(mt());
-        const float uy = u24(mt());
-        px[j] = ux * 400.0f;
-        py[j] = uy * 100.0f;
+// `count` formations' reset draws (simulate.py:133-143: per formation N (x, y) pairs, then the
+// goal pair) from the stream's current position, in chunks of ~48K draws (an L2-resident
+// buffer): a chunk's draws in one fill, then each formation's values in one pass.  With `at`,
+// also each value's staging tag for generation `gen` (fenv_internal.h), taken while the bits
+// are in registers.
+void draw_formations(Mt19937 &mt, int64_t N, int64_t count, float *px, float *py, float *gx,
+                     float *gy, uint32_t gen = 0, uint32_t *at = nullptr, uint32_t *gt = nullptr) {
+    const int64_t per = 2 * N + 2;
+    const int64_t chunk = std::max<int64_t>(1, 49152 / per);
+    std::vector<uint32_t> u((size_t)(std::min<int64_t>(chunk, std::max<int64_t>(count, 1)) * per));
+    for (int64_t f0 = 0; f0 < count; f0 += chunk) {
+        const int64_t cnt = std::min<int64_t>(chunk, count - f0);
+        mt.fill(u.data(), (size_t)(cnt * per));
+        for (int64_t i = 0; i < cnt; ++i) {
+            const uint32_t *r = u.data() + i * per;
+            const int64_t f = f0 + i;
+            for (int64_t j = 0; j < N; ++j) {
+                const int64_t a = f * N + j;
+                const float x = u24(r[2 * j]) * 400.0f, y = u24(r[2 * j + 1]) * 100.0f;
+                px[a] = x;
+                py[a] = y;
+                if (at) {
+                    uint32_t bx, by;
+                    std::memcpy(&bx, &x, 4);
+                    std::memcpy(&by, &y, 4);
+                    at[a] = fenvk::stage_tag_agent(gen, a, bx, by);
+                }
+            }
+            const float g0 = u24(r[2 * N]) * 280.0f + 60.0f;
+            const float g1 = u24(r[2 * N + 1]) * 480.0f + 60.0f;
+            gx[f] = g0;
+            gy[f] = g1;
+            if (gt) {
+                uint32_t bx, by;
+                std::memcpy(&bx, &g0, 4);
+                std::memcpy(&by, &g1, 4);
+                gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
+            }
+        }
     }
-    const float g0 = u24(mt());
-    const float g1 = u24(mt());
-    gx = g0 * 280.0f + 60.0f;
-    gy = g1 * 480.0f + 60.0f;
 }
 
 // Device frees the runtime refused because a stream capture was under way (a hipFree inside a
@@ -331,21 +355,8 @@ struct fenv {
         const uint64_t per = 2ull * (uint64_t)c.N + 2ull;
         mt.discard(per * (uint64_t)c.f0);
         float *hp = hpend + off;
-        float *px = hp, *py = hp + A, *gx = hp + 2 * A, *gy = hp + 2 * A + c.F;
-        uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F), *gt = at + A;
-        for (int64_t f = 0; f < c.F; ++f) {
-            draw_formation(mt, c.N, px + f * c.N, py + f * c.N, gx[f], gy[f]);
-            for (int64_t a = f * c.N; a < (f + 1) * c.N; ++a) {
-                uint32_t bx, by;
-                std::memcpy(&bx, px + a, 4);
-                std::memcpy(&by, py + a, 4);
-                at[a] = fenvk::stage_tag_agent(gen, a, bx, by);
-            }
-            uint32_t bx, by;
-            std::memcpy(&bx, gx + f, 4);
-            std::memcpy(&by, gy + f, 4);
-            gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
-        }
+        uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F);
+        draw_formations(mt, c.N, c.F, hp, hp + A, hp + 2 * A, hp + 2 * A + c.F, gen, at, at + A);
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
     }
 
@@ -822,8 +833,7 @@ int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64
     mt.seed(seed);
     const uint64_t per = 2ull * (uint64_t)num_agents + 2ull;
     mt.discard(per * ((uint64_t)skip_sets * (uint64_t)total + (uint64_t)first));
-    for (int64_t f = 0; f < count; ++f)
-        draw_formation(mt, num_agents, px + f * num_agents, py + f * num_agents, gx[f], gy[f]);
+    draw_formations(mt, num_agents, count, px, py, gx, gy);
     return FENV_OK;
 }
 
