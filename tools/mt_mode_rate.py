@@ -3,7 +3,8 @@ BASELINE config 3 (1,048,576 x 5) or the size given, over a window that holds re
 (episode = 1002 steps).  MT19937 mode draws every reset set on the host (std::mt19937 replay of
 torch's global stream): what that costs the rollout is the difference between the two lines.
 
-    python tools/mt_mode_rate.py [formations] [steps]      -> one JSON line per mode
+    python tools/mt_mode_rate.py [formations] [steps] [modes]   -> one JSON line per mode
+                                                                (modes: philox,mt19937)
 """
 import json
 import os
@@ -24,7 +25,8 @@ F = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 3010
 N, T = 5, 10
 
-for mode in ("philox", "mt19937"):
+MODES = sys.argv[3].split(",") if len(sys.argv) > 3 else ["philox", "mt19937"]
+for mode in MODES:
     env = ve.FormationEnv({"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": True},
                           log=False, device=DEV, seed=0, reset_mode=mode)
     A = env.num_envs
