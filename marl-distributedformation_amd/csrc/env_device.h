@@ -87,16 +87,22 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
                                            int64_t a, int i, uint32_t ep_new, float &px,
                                            float &py, float &gx, float &gy) {
     if (MODE == FENV_RESET_MT19937) {
+        // indices laundered here: a and f are loop-invariant in the kernels' step loops, so the
+        // compiler would otherwise hoist the six addresses below (12 VGPRs) out of the loop for
+        // this rarely taken branch -- one occupancy step down on every MT19937 kernel
+        int64_t la = a, lf = f;
+        asm volatile("" : "+v"(la));
+        asm volatile("" : "+v"(lf));
         const int64_t A = c.F * (int64_t)c.N;
-        px = p.pend[a];
-        py = p.pend[A + a];
-        gx = p.pend[2 * A + f];
-        gy = p.pend[2 * A + c.F + f];
+        px = p.pend[la];
+        py = p.pend[A + la];
+        gx = p.pend[2 * A + lf];
+        gy = p.pend[2 * A + c.F + lf];
         // the tags of the lane's draws (a lane owning no agent -- env_step's `live` -- may index
         // past the set; it applies nothing, so it is not checked there)
         if (f < c.F && a < A) {
             const uint32_t *tg = reinterpret_cast<const uint32_t *>(p.pend + 2 * A + 2 * c.F);
-            const uint32_t ta = tg[a], tf = tg[A + f];
+            const uint32_t ta = tg[la], tf = tg[A + lf];
             const uint32_t bx = __float_as_uint(px), by = __float_as_uint(py);
             if (ta != stage_tag_agent(p.gen, a, bx, by))
                 stage_tag_fail(p, f, a, ta, bx, by);
