@@ -45,6 +45,14 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 // of libstdc++'s per-draw generator (§9.2).  Pinned bit for bit to the oracle's
 // MT19937 by tests/test_oracle_golden.py (fenv_host_reset_draws) and to the reference's draws
 // by the golden fixtures.
+// Host-only hot loops (the MT19937 replay) get an AVX2 clone beside the baseline x86-64 one,
+// picked at load time by the CPU.  hipcc also runs a device pass over this file, which has no
+// multiversioning (and emits none of these host functions).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FENV_HOST_CLONES
+#else
+#define FENV_HOST_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
 class Mt19937 {
     static constexpr int kN = 624, kM = 397;
     uint32_t s_[kN];
@@ -59,7 +67,7 @@ class Mt19937 {
         y ^= (y << 15) & 0xEFC60000u;
         return y ^ (y >> 18);
     }
-    void twist() {
+    FENV_HOST_CLONES void twist() {
         for (int i = 0; i < kN - kM; ++i) s_[i] = tw(s_[i], s_[i + 1], s_[i + kM]);
         for (int i = kN - kM; i < kN - 1; ++i) s_[i] = tw(s_[i], s_[i + 1], s_[i + kM - kN]);
         s_[kN - 1] = tw(s_[kN - 1], s_[0], s_[kM - 1]);
@@ -75,7 +83,7 @@ class Mt19937 {
         pos_ = kN;
     }
     // the next n draws into d[0..n), tempered straight from the state a block at a time
-    void fill(uint32_t *d, size_t n) {
+    FENV_HOST_CLONES void fill(uint32_t *d, size_t n) {
         while (n) {
             if (pos_ == kN) twist();
             const size_t k = std::min<size_t>(n, (size_t)(kN - pos_));
@@ -99,11 +107,43 @@ class Mt19937 {
 // torch.rand float32 from one 32-bit MT19937 draw.
 inline float u24(uint32_t r) { return (float)(r & 0xFFFFFFu) * 0x1.0p-24f; }
 
-// `count` formations' reset draws (simulate.py:133-143: per formation N (x, y) pairs, then the
-// goal pair) from the stream's current position, in chunks of ~48K draws (an L2-resident
-// buffer): a chunk's draws in one fill, then each formation's values in one pass.  With `at`,
-// also each value's staging tag for generation `gen` (fenv_internal.h), taken while the bits
-// are in registers.
+// Formations [f0, f0 + cnt) from their draws u[cnt * (2N + 2)] (simulate.py:133-143: per
+// formation N (x, y) pairs, then the goal pair), with each value's staging tag for generation
+// `gen` when `at` is given (fenv_internal.h), taken while the bits are in registers.
+FENV_HOST_CLONES void formations_from_draws(const uint32_t *u, int64_t f0, int64_t cnt, int64_t N,
+                                            float *px, float *py, float *gx, float *gy,
+                                            uint32_t gen, uint32_t *at, uint32_t *gt) {
+    const int64_t per = 2 * N + 2;
+    for (int64_t i = 0; i < cnt; ++i) {
+        const uint32_t *r = u + i * per;
+        const int64_t f = f0 + i;
+        for (int64_t j = 0; j < N; ++j) {
+            const int64_t a = f * N + j;
+            const float x = u24(r[2 * j]) * 400.0f, y = u24(r[2 * j + 1]) * 100.0f;
+            px[a] = x;
+            py[a] = y;
+            if (at) {
+                uint32_t bx, by;
+                std::memcpy(&bx, &x, 4);
+                std::memcpy(&by, &y, 4);
+                at[a] = fenvk::stage_tag_agent(gen, a, bx, by);
+            }
+        }
+        const float g0 = u24(r[2 * N]) * 280.0f + 60.0f;
+        const float g1 = u24(r[2 * N + 1]) * 480.0f + 60.0f;
+        gx[f] = g0;
+        gy[f] = g1;
+        if (gt) {
+            uint32_t bx, by;
+            std::memcpy(&bx, &g0, 4);
+            std::memcpy(&by, &g1, 4);
+            gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
+        }
+    }
+}
+
+// `count` formations' reset draws from the stream's current position, in chunks of ~48K draws
+// (an L2-resident buffer): a chunk's draws in one fill, then its formations in one pass.
 void draw_formations(Mt19937 &mt, int64_t N, int64_t count, float *px, float *py, float *gx,
                      float *gy, uint32_t gen = 0, uint32_t *at = nullptr, uint32_t *gt = nullptr) {
     const int64_t per = 2 * N + 2;
@@ -112,32 +152,7 @@ void draw_formations(Mt19937 &mt, int64_t N, int64_t count, float *px, float *py
     for (int64_t f0 = 0; f0 < count; f0 += chunk) {
         const int64_t cnt = std::min<int64_t>(chunk, count - f0);
         mt.fill(u.data(), (size_t)(cnt * per));
-        for (int64_t i = 0; i < cnt; ++i) {
-            const uint32_t *r = u.data() + i * per;
-            const int64_t f = f0 + i;
-            for (int64_t j = 0; j < N; ++j) {
-                const int64_t a = f * N + j;
-                const float x = u24(r[2 * j]) * 400.0f, y = u24(r[2 * j + 1]) * 100.0f;
-                px[a] = x;
-                py[a] = y;
-                if (at) {
-                    uint32_t bx, by;
-                    std::memcpy(&bx, &x, 4);
-                    std::memcpy(&by, &y, 4);
-                    at[a] = fenvk::stage_tag_agent(gen, a, bx, by);
-                }
-            }
-            const float g0 = u24(r[2 * N]) * 280.0f + 60.0f;
-            const float g1 = u24(r[2 * N + 1]) * 480.0f + 60.0f;
-            gx[f] = g0;
-            gy[f] = g1;
-            if (gt) {
-                uint32_t bx, by;
-                std::memcpy(&bx, &g0, 4);
-                std::memcpy(&by, &g1, 4);
-                gt[f] = fenvk::stage_tag_goal(gen, f, bx, by);
-            }
-        }
+        formations_from_draws(u.data(), f0, cnt, N, px, py, gx, gy, gen, at, gt);
     }
 }
 
