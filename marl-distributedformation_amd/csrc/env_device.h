@@ -382,43 +382,6 @@ __device__ __forceinline__ void store_obs_rows(float *stage, const float (&o)[8]
     __builtin_amdgcn_wave_barrier();
 }
 
-// store_obs_rows for D = 8 and a 16-B-aligned destination as exactly two range-checked buffer
-// stores per wave, with no branch: lanes past the wave's M rows address bytes past the buffer
-// record's num_records (= M * 32) and the hardware drops them.  A step then issues the same
-// number of vector-memory instructions on every path, so the compiler can wait for the next
-// step's action load with vmcnt(2) -- the two stores stay in flight -- instead of the vmcnt(0)
-// that a path-dependent store count forces (which made every step wait for its stores' write
-// acknowledgements: the rollout's latency coupling to HBM).
-template <bool NT>
-__device__ __forceinline__ void store_obs_rows_buf(float *stage, const float (&o)[8], int lane,
-                                                   int M, float *dst) {
-    stage_obs_rows<8>(stage, o, lane);
-    __builtin_amdgcn_wave_barrier();
-    // wave-uniform by construction; readfirstlane lets the compiler keep the descriptor in
-    // SGPRs (no waterfall loop)
-    const uint64_t da = reinterpret_cast<uint64_t>(dst);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)da);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(da >> 32));
-    float *dstu = reinterpret_cast<float *>(((uint64_t)hi << 32) | lo);
-    const int nrec = __builtin_amdgcn_readfirstlane(M * 32);
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(dstu, (short)0, nrec, 0x00020000);
-    constexpr int kAux = NT ? 2 : 0;  // gfx950 cache policy: nt
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int q = lane + 64 * k;
-        const float4 v = reinterpret_cast<const float4 *>(stage)[q];
-        u32x4 b;
-        b.x = __float_as_uint(v.x);
-        b.y = __float_as_uint(v.y);
-        b.z = __float_as_uint(v.z);
-        b.w = __float_as_uint(v.w);
-        __builtin_amdgcn_raw_buffer_store_b128(b, r, q * 16, 0, kAux);
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
 #ifndef FENV_WAVE_SUM_DPP
 #define FENV_WAVE_SUM_DPP 1
 #endif

@@ -41,52 +41,14 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
 #ifndef FENV_RS_PF
 #define FENV_RS_PF 1
 #endif
-// observation rows as branch-free range-checked buffer stores (store_obs_rows_buf) in the staged
-// kernel when obs is 16-B aligned and D = 8
-#ifndef FENV_RS_OB
-#define FENV_RS_OB 0
-#endif
 // Register budget: left to the compiler (75 VGPRs -> 6 waves/SIMD, 3 workgroups per CU).  Forcing
 // 64 VGPRs (4 workgroups per CU) spills and runs ~12 % slower (tools/env_ab.sh).
 #ifndef FENV_RS_OCC
 #define FENV_RS_OCC
 #endif
-// XCD-aware slice order (FENV_RS_XCD=1): workgroups are dispatched round-robin over the 8 XCDs
-// (block b -> XCD b % 8), so by default neighbouring slices -- whose 480-B done rows share
-// 128-B lines -- sit in different XCDs' L2s.  The remap gives each XCD one contiguous range of
-// slices (blocks b, b + 8, b + 16, ... -> consecutive slices).
-#ifndef FENV_RS_XCD
-#define FENV_RS_XCD 0
-#endif
-// Occupancy probe (FENV_RS_PAD bytes of extra LDS per workgroup caps the resident workgroups per
-// CU: A/B builds only, 0 in the product).
-#ifndef FENV_RS_PAD
-#define FENV_RS_PAD 0
-#endif
-__device__ __forceinline__ int64_t xcd_slice(int64_t b, int64_t nb) {
-    if (!FENV_RS_XCD) return b;
-    const int64_t x = b & 7, q = nb >> 3, r = nb & 7;
-    return x * q + (x < r ? x : r) + (b >> 3);
-}
 constexpr int kRS = 8;
 constexpr int kRSA = 64 * kRS;
 constexpr int kRSTB = FENV_RS_TB;
-
-// Address-translation prefetch (round 3, FENV_XPF; tools/xlat_probe.py).  A 10-step
-// launch at config 3 writes ~2.5 GB of output planes: ~1,250 2-MiB pages per launch, more than the
-// translation cache keeps between launches, so the first touch of every page by every XCD waits
-// for a page walk, and the CUs' in-flight translations pile up (TCP_CLIENT_UTCL1_INFLIGHT 2.7x the
-// 1-GB-footprint launch's per byte).  Wave 0 of workgroup b touches, during its step 0, the pages
-// that workgroup b + FENV_XPF_LA (same XCD: LA is a multiple of 8) will write or read, once per
-// (XCD, page): one 4-B load per new page per stream and plane, its value unused (kept live to the
-// end of the wave so its register is not reused before it lands).
-#ifndef FENV_XPF
-#define FENV_XPF 0
-#endif
-#ifndef FENV_XPF_LA
-#define FENV_XPF_LA 832
-#endif
-static_assert(FENV_XPF_LA % 8 == 0, "the prefetch target must sit on the prefetching XCD");
 
 struct RSStage {
     float *rbuf;    // [kRSTB][kRSA]
@@ -94,36 +56,7 @@ struct RSStage {
     int li;         // this lane's slot in the slice (w * agents-per-wave + lane)
     int nwg;        // agents in the slice
     int64_t g0;     // first agent of the slice
-    int64_t blk;    // this workgroup's slice index
-    int64_t nblk;   // slices in the grid
-    int64_t span;   // agents per full slice
 };
-
-// One lane per (stream, plane): lane j -> stream j & 3 (obs, act, rew, done), plane j >> 2.  Returns
-// the loaded word (0 for lanes with nothing to touch); the caller keeps it live.
-template <int D>
-__device__ __forceinline__ uint32_t xlat_touch(const RSStage &r, int64_t A, int32_t T,
-                                               const float2 *act, const float *obs,
-                                               const float *rew, const uint8_t *done) {
-    const int lane = threadIdx.x & 63;
-    const int sidx = lane & 3, k = lane >> 2;
-    const int64_t bt = r.blk + FENV_XPF_LA;
-    if (k >= T || bt >= r.nblk) return 0u;
-    const char *base = sidx == 0 ? reinterpret_cast<const char *>(obs)
-                     : sidx == 1 ? reinterpret_cast<const char *>(act)
-                     : sidx == 2 ? reinterpret_cast<const char *>(rew)
-                                 : reinterpret_cast<const char *>(done);
-    const int64_t esz = sidx == 0 ? 4 * D : sidx == 1 ? 8 : sidx == 2 ? 4 : 1;
-    if (base == nullptr) return 0u;
-    // the page of the last byte of slice bt, unless slice bt - 8 (the same XCD's previous slice)
-    // already ended in it
-    const int64_t e1 = (bt + 1) * r.span < A ? (bt + 1) * r.span : A;
-    const int64_t e0 = (bt - 7) * r.span < A ? (bt - 7) * r.span : A;
-    const uintptr_t last = reinterpret_cast<uintptr_t>(base + ((int64_t)k * A + e1) * esz - 1);
-    const uintptr_t prev = reinterpret_cast<uintptr_t>(base + ((int64_t)k * A + e0) * esz - 1);
-    if ((last >> 21) == (prev >> 21)) return 0u;
-    return __builtin_nontemporal_load(reinterpret_cast<const uint8_t *>(last));
-}
 
 // rows [kfirst, kfirst + nrows) of the slice from the LDS buffers (all kRSA threads).  Vector
 // path: thread (c4 = tid & 127, tid >> 7) stores 16 B of reward / 4 B of done per row, 4 rows per
@@ -168,8 +101,7 @@ __device__ __forceinline__ void rs_flush(const RSStage &r, int kfirst, int nrows
 // profiles/ab/r3_config1_split3_ab.txt; source at commit 2c54623.)
 constexpr int kRoleAll = 0, kRoleState = 1, kRoleObs = 2;
 
-template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll, bool NT = false,
-          bool OB = false>
+template <int D, int MODE, bool RA, bool RS, int PF, class X, int ROLE = kRoleAll, bool NT = false>
 __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st,
                                              const DevPending &p, const X &x, bool active,
                                              int64_t f, int64_t a, int i, float *stage, int lane,
@@ -201,9 +133,7 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
     // staged rows: FENV_RS_PF steps (the chunk loop below is unrolled by it); in-kernel actions:
     // one step
     constexpr int kPF = RA ? 1 : (RS ? FENV_RS_PF : PF);
-    static_assert(!OB || D == 8, "buffer-store observation rows are the D = 8 layout");
     float2 ring[kPF];
-    uint32_t xpf = 0u;  // translation-prefetch word (FENV_XPF), consumed at the end
     const int64_t ga = c.f0 * c.N + a;  // global agent index (shard-invariant actions)
     uint4 words = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -225,19 +155,12 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
         } else if (active && k + kPF < T) {
             ring[j] = act[(int64_t)(k + kPF) * A + a];
         }
-        // after the next step's action load: the next wait on that load does not wait for this
-        if (FENV_XPF && RS && k == 0 && threadIdx.x < 64)
-            xpf = xlat_touch<D>(rsg, A, T, act, obs, rew, done);
         float rw;
         bool dn, rs;
         env_step<MODE, X, !kObsR>(c, p, x, f, a, i, active, ac, s, rw, dn, rs);
         any_reset |= rs;
         const int64_t row = (int64_t)k * A + a;
-        if constexpr (OB) {  // obs non-NULL and 16-B aligned (the launcher checks)
-            float o[8];
-            env_obs<D>(x, s, o);
-            store_obs_rows_buf<NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
-        } else if (ROLE != kRoleState && obs) {
+        if (ROLE != kRoleState && obs) {
             float o[8];
             env_obs<D>(x, s, o);
             store_obs_rows<D, NT>(stage, o, lane, M, obs + ((int64_t)k * A + a_first) * D);
@@ -284,7 +207,6 @@ __device__ __forceinline__ void rollout_body(const Consts &c, const DevState &st
             }
         }
     }
-    if (FENV_XPF && RS) asm volatile("" ::"v"(xpf));  // the prefetch has landed before exit
     if (!kObsR && active) {
         st.px[a] = s.px;
         st.py[a] = s.py;
@@ -401,7 +323,7 @@ __global__ __launch_bounds__(512) void k_rollout_wave_split(Consts c, DevState s
     }
 }
 
-template <int D, int MODE, bool RA, bool NT, bool OB = false>
+template <int D, int MODE, bool RA, bool NT>
 __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, DevState st, DevPending p,
                                                           int32_t T,
                                                           const float2 *__restrict__ act,
@@ -416,12 +338,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     __shared__ __attribute__((aligned(16))) float rbuf[kRSTB * kRSA];
     __shared__ __attribute__((aligned(16))) uint8_t dbuf[kRSTB * kRSA];
     __shared__ float2 red[kRS];
-#if FENV_RS_PAD > 0
-    __shared__ char rs_pad[FENV_RS_PAD];
-    if (T < 0) rs_pad[threadIdx.x] = 0;  // never taken (T >= 0): keeps the allocation
-#endif
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t blk = xcd_slice(blockIdx.x, gridDim.x);
+    const int64_t blk = blockIdx.x;
     const int64_t wave = blk * kRS + w;
     const int N = c.N;
     const int Mw = c.fpw * N;  // agents of a full wave
@@ -441,11 +359,8 @@ __global__ __launch_bounds__(kRSA) FENV_RS_OCC void k_rollout_wave_rs(Consts c, 
     rsg.li = w * Mw + lane;
     rsg.g0 = blk * kRS * Mw;
     rsg.nwg = (int)((A - rsg.g0) < (int64_t)kRS * Mw ? (A - rsg.g0) : (int64_t)kRS * Mw);
-    rsg.blk = blk;
-    rsg.nblk = gridDim.x;
-    rsg.span = (int64_t)kRS * Mw;
     float rsum = 0.f, dsum = 0.f;
-    rollout_body<D, MODE, RA, true, 1, WaveX, kRoleAll, NT, OB>(c, st, p, x, active, f, a, i, stage[w],
+    rollout_body<D, MODE, RA, true, 1, WaveX, kRoleAll, NT>(c, st, p, x, active, f, a, i, stage[w],
                                                            lane, M,
                                        f_first * N, T, act, gen, obs, rew, done, rsum, dsum, rsg);
     if (partial) {  // one {sum reward, sum done} record per 4 waves -- the same records, in the
@@ -516,14 +431,6 @@ __global__ __launch_bounds__(1024) void k_rollout_block(Consts c, DevState st, D
     }
 }
 
-// Workgroup-staged A/B variant (k_rollout_wg): source in tools/ab/k_rollout_wg.inc, compiled
-// in only with -DFENV_RW=1 (not in the product library).
-#ifndef FENV_RW
-#define FENV_RW 0
-#endif
-#if FENV_RW
-#include "../../tools/ab/k_rollout_wg.inc"
-#endif
 
 // ---------------------------------------------------------------- reset + observe
 template <int D, int MODE, bool RESET, class X>
@@ -807,9 +714,6 @@ static inline bool use_split(const Consts &c) {
 }
 
 int64_t rollout_group_count(const Consts &c) {
-#if FENV_RW
-    if (wave_path(c.N)) return ((c.F + c.fpw - 1) / c.fpw + kRW - 1) / kRW;
-#endif
     return group_count(c);
 }
 
@@ -841,23 +745,10 @@ static hipError_t rollout_dmn(const Consts &c, const DevState &s, const DevPendi
         return hipGetLastError();
     }
     const ActGen g0{};
-#if FENV_RW
-    if (wave_path(c.N)) {
-        hipLaunchKernelGGL((k_rollout_wg<D, MODE>), dim3((unsigned)rollout_group_count(c)),
-                           dim3(64 * kRW), RWLds::bytes(D), st, c, s, p, T, a2, obs, rew, done, p2,
-                           accum);
-        return hipGetLastError();
-    }
-#endif
     if (use_rs(c, T)) {
-        if (FENV_RS_OB && D == 8 && obs && (reinterpret_cast<uintptr_t>(obs) & 15) == 0)
-            hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false, NT, D == 8>),
-                               dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
-                               a2, g0, obs, rew, done, p2, accum);
-        else
-            hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false, NT>),
-                               dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T,
-                               a2, g0, obs, rew, done, p2, accum);
+        hipLaunchKernelGGL((k_rollout_wave_rs<D, MODE, false, NT>),
+                           dim3((unsigned)rs_blocks(c)), dim3(kRSA), 0, st, c, s, p, T, a2, g0,
+                           obs, rew, done, p2, accum);
     } else if (use_split(c)) {
         const unsigned blocks = (unsigned)group_count(c);
         if (use_pf(c, T))
@@ -919,9 +810,6 @@ static hipError_t rollout_dm(const Consts &c, const DevState &s, const DevPendin
 }
 
 const char *rollout_kernel_name(const Consts &c, int32_t T) {
-#if FENV_RW
-    if (wave_path(c.N)) return "k_rollout_wg";
-#endif
     if (large_path(c.N)) return "k_rollout_large";
     if (use_rs(c, T)) return "k_rollout_wave_rs";
     if (use_split(c))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B builds of libfenv.so from the current sources: build_variants/libfenv_<tag>.so for each
-# "tag:flags" argument (e.g. "ob:-DFENV_RS_OB=1").  Built here (CPU), shipped with the tree.
+# "tag:flags" argument (e.g. "nosplit:-DFENV_SPLIT=0").  Built here (CPU), shipped with the tree.
 set -eu
 R="$(cd "$(dirname "$0")/.." && pwd)"
 cd "$R/marl-distributedformation_amd/csrc"
