@@ -14,6 +14,10 @@ reward / done for every step into a device rollout buffer, with the actions read
 (inputs resident before the timed region).  Episode stats are reduced on device and all-reduced
 over RCCL every --stats-every rollouts on a side stream.
 
+Secondary lines (N = 1, after the timed region): the fused policy rollout (config 2), the PPO
+update, MT19937 reset mode, the random-action launch, the numpy (PCIe-inclusive) face, configs
+1 and 4, the single-step face, and the CPU baseline.
+
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
@@ -351,6 +355,44 @@ def numpy_face_bench(pkgname: str, dev, formations: int, agents: int, steps: int
                         f"x {steps}", "value": A * steps / el, "unit": "agent-steps/s",
             "ms_per_step": 1e3 * el / steps, "pcie_bytes_per_step": pcie_b,
             "pcie_gbs": pcie_b * steps / el / 1e9}
+
+
+def mt_mode_bench(pkgname: str, dev, formations: int, agents: int, steps: int = 2100,
+                  T: int = 10) -> dict:
+    """The same fused rollouts in MT19937 reset mode (the reference's exact RNG stream: every
+    reset set replayed on the host and staged), over a window holding two reset
+    events (episode = 1,002 steps), with the Philox rate of the same window beside it."""
+    import torch
+    from importlib import import_module
+    venv = import_module(pkgname + ".vectorized_env")
+    out = {"workload": f"{formations} formations x {agents} agents, fused {T}-step rollouts, "
+                       f"{steps} steps (two reset events), aligned episodes", "unit": "agent-steps/s"}
+    for mode in ("mt19937", "philox"):
+        cfg = {"num_formation": formations, "num_agents_per_formation": agents, "goal_in_obs": True}
+        env = venv.FormationEnv(cfg, log=False, device=dev, seed=0, reset_mode=mode)
+        A = env.num_envs
+        acts = torch.rand((T, A, 2), device=dev) * 2 - 1
+        obs = torch.empty((T, A, 8), device=dev)
+        rew = torch.empty((T, A), device=dev)
+        done = torch.empty((T, A), dtype=torch.bool, device=dev)
+        env.reset_tensor()
+        for _ in range(3):
+            env.rollout(acts, obs, rew, done)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        k = 0
+        while k < steps:
+            L = min(T, steps - k)
+            env.rollout(acts[:L], obs[:L], rew[:L], done[:L])
+            k += L
+        torch.cuda.synchronize()
+        out[mode] = A * steps / (time.perf_counter() - t0)
+        env.release()
+        del env, acts, obs, rew, done
+        torch.cuda.empty_cache()
+    out["value"] = out["mt19937"]
+    out["mt19937_over_philox"] = out["mt19937"] / out["philox"]
+    return out
 
 
 def secondary(fn, *a):
@@ -799,6 +841,7 @@ def main():
             out["numpy_face"] = {
                 "config0": secondary(numpy_face_bench, pkg.__name__, dev, 1000, N, 200),
                 "config3": secondary(numpy_face_bench, pkg.__name__, dev, args.formations, N, 10)}
+            out["mt19937_mode"] = secondary(mt_mode_bench, pkg.__name__, dev, args.formations, N)
             out["random_action_rollout"] = random_action_bench(pkg.__name__, dev,
                                                                args.formations, N)
             out["env_configs"] = {"config1": env_config_bench(pkg.__name__, dev, 4096, 5, 400),
