@@ -131,11 +131,7 @@ __device__ __forceinline__ void draw_reset(const Consts &c, const DevPending &p,
 
 // ---------------------------------------------------------------- ring-neighbour exchange
 // Three exchange rounds per env step: A {px,py}->prev,next, C {ind}->prev,next, D {nx,ny}->
-// prev,next.  FENV_XA=0 (A/B builds) restores round 1's four: A {px,py}->next, B {drr}->prev
-// (the left distance taken as the right distance of agent i-1), C, D.
-#ifndef FENV_XA
-#define FENV_XA 1
-#endif
+// prev,next (round 1 had four: A {px,py}->next, B {drr}->prev, C, D).
 
 struct WaveX {  // N <= 64: lanes of one formation are contiguous in the wavefront
     int lp, ln;
@@ -143,7 +139,6 @@ struct WaveX {  // N <= 64: lanes of one formation are contiguous in the wavefro
         un = __shfl(u, ln, 64);
         vn = __shfl(v, ln, 64);
     }
-    __device__ __forceinline__ float b_prev(float v) const { return __shfl(v, lp, 64); }
     __device__ __forceinline__ void a_pn(float u, float v, float &up, float &un, float &vp,
                                          float &vn) const {
         up = __shfl(u, lp, 64);
@@ -188,11 +183,6 @@ struct BlockX {
         un = lds[0 * kMaxN + in];
         vp = lds[1 * kMaxN + ip];
         vn = lds[1 * kMaxN + in];
-    }
-    __device__ __forceinline__ float b_prev(float v) const {
-        lds[2 * kMaxN + i] = v;
-        __syncthreads();
-        return lds[2 * kMaxN + ip];
     }
     __device__ __forceinline__ void c_pn(float v, float &vp, float &vn) const {
         lds[3 * kMaxN + i] = v;
@@ -243,19 +233,12 @@ __device__ __forceinline__ void env_step(const Consts &c, const DevPending &p, c
 
     // compute_reward_and_done, simulate.py:180-211
     const float dg = norm2(s.px - s.gx, s.py - s.gy);
-#if FENV_XA
     // one exchange round for both neighbours' positions; both distances computed here as the
     // reference does (:197-198: norm(p - roll(p, -1)), norm(p - roll(p, 1)))
     float ppx, pnx, ppy, pny;
     x.a_pn(s.px, s.py, ppx, pnx, ppy, pny);
     const float drr = norm2(s.px - pnx, s.py - pny);  // ||p_i - p_{i+1}||  (:197)
     const float drl = norm2(s.px - ppx, s.py - ppy);  // ||p_i - p_{i-1}||  (:198)
-#else
-    float pnx, pny;
-    x.a_next(s.px, s.py, pnx, pny);
-    const float drr = norm2(s.px - pnx, s.py - pny);  // ||p_i - p_{i+1}||  (:197)
-    const float drl = x.b_prev(drr);                  // ||p_i - p_{i-1}|| == drr_{i-1} bitwise
-#endif
     const float ctg = dg < 100.0f ? 10.0f : 0.0f;     // :183-187
     const float rd = -0.1f * dg;                      // :191
     const float rr = nb_reward(drr - c.d_nb);         // :202-205
@@ -382,14 +365,10 @@ __device__ __forceinline__ void store_obs_rows(float *stage, const float (&o)[8]
     __builtin_amdgcn_wave_barrier();
 }
 
-#ifndef FENV_WAVE_SUM_DPP
-#define FENV_WAVE_SUM_DPP 1
-#endif
 // Sum over the 64 lanes, returned in every lane.  DPP form: row_shr 1/2/4/8 inside each 16-lane
 // row, then row_bcast 15 / 31 carry the row sums up, so lane 63 holds the total (a fixed order:
 // deterministic), read back with v_readlane.  Six VALU ops instead of six LDS-latency swizzles.
 __device__ __forceinline__ float wave_sum(float v) {
-#if FENV_WAVE_SUM_DPP
     int x = __float_as_int(v);
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
@@ -398,11 +377,6 @@ __device__ __forceinline__ float wave_sum(float v) {
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false)));
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false)));
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
-#else
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
-#endif
 }
 
 }  // namespace fenvk

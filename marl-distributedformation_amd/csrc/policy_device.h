@@ -49,9 +49,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef FENV_SPLIT_MIX
-#define FENV_SPLIT_MIX 1
-#endif
 #ifndef FENV_POLICY_PRIO
 #define FENV_POLICY_PRIO 0
 #endif
@@ -100,9 +97,6 @@ constexpr int kPolicyLds = oSc + 12;       // 10,700 floats = 42.8 KB
 
 // x = hi + lo: hi = x truncated to 11 significant bits (exact in f16 for 2^-14 <= |x| < 65504),
 // lo = f16(x - hi) (x - hi is exact).  Two values per v_cvt_pkrtz_f16_f32.
-__device__ __forceinline__ float hi11(float x) {
-    return __uint_as_float(__float_as_uint(x) & 0xFFFFE000u);
-}
 __device__ __forceinline__ uint32_t pk_rtz(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
 }
@@ -122,17 +116,6 @@ __device__ __forceinline__ void split8(const V &v, int base, h8 &hi, h8 &lo) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const float x = v[base + 2 * p], y = v[base + 2 * p + 1];
-#if FENV_SPLIT_MIX == 2
-        // hi = RTZ to f16; lo = f16(x - f32(hi)) computed AND packed by v_fma_mix{lo,hi}_f16
-        // (f16 operand, f32 math, one rounding to f16): 3 instructions per pair instead of 4
-        const uint32_t hh = pk_rtz(x, y);
-        uint32_t ll;
-        asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(ll) : "v"(hh), "v"(x));
-        asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "+v"(ll) : "v"(hh), "v"(y));
-        H[p] = hh;
-        L[p] = ll;
-#elif FENV_SPLIT_MIX
         // hi = RTZ to f16 (the 11 leading significant bits); the exact remainder x - f32(hi)
         // straight from the packed halves with v_fma_mix_f32 (f16 operand, f32 math)
         const uint32_t hh = pk_rtz(x, y);
@@ -142,11 +125,6 @@ __device__ __forceinline__ void split8(const V &v, int base, h8 &hi, h8 &lo) {
             : "=v"(ly) : "v"(hh), "v"(y));
         H[p] = hh;
         L[p] = pk_rtz(lx, ly);
-#else
-        const float xh = hi11(x), yh = hi11(y);
-        H[p] = pk_rtz(xh, yh);
-        L[p] = pk_rtz(x - xh, y - yh);
-#endif
     }
     hi = __builtin_bit_cast(h8, H);
     lo = __builtin_bit_cast(h8, L);

@@ -228,16 +228,12 @@ __global__ __launch_bounds__(64 * kPRWaves) FENV_PR_OCCUPANCY void k_policy_roll
         policy_rollout_unit<D, MODE>(c, st, p, g, wimg, stage_all[w], wave * c.fpw);
 }
 
-#ifndef FENV_PR_PERSISTENT
-#define FENV_PR_PERSISTENT 1  // 0: one wave-unit per wave (a workgroup per 4 units), A/B
-#endif
-
 template <int D, int MODE>
 static hipError_t policy_rollout_dm(const Consts &c, const DevState &s, const DevPending &p,
                                     const PRArgs &g, hipStream_t st) {
     const int64_t waves = (c.F + c.fpw - 1) / c.fpw;
     int64_t blocks = (waves + kPRWaves - 1) / kPRWaves;
-    if (FENV_PR_PERSISTENT) {
+    {
         // resident workgroups, per template instance (D, MODE) and device (devices may differ)
         static std::atomic<int> resident_by_dev[64];
         int dev = 0;
