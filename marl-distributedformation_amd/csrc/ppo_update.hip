@@ -148,29 +148,18 @@ constexpr int kPerTS = 20;  // parameters owned per thread, split launch (actor:
 // tanh x = 1 - 2 / (1 + e^(2x)) on v_exp_f32 + v_rcp_f32 (absolute error < 3e-7 over the whole
 // range, +-1 at +-inf) instead of the ~30-instruction libm tanhf: the update's forward only has
 // to match torch's tanh to fp32 rounding noise (tests/test_gpu_rollout.py bounds the update)
-#ifndef FENV_PPO_FAST_TANH
-#define FENV_PPO_FAST_TANH 1
-#endif
 __device__ __forceinline__ float tanh_u(float x) {
-#if FENV_PPO_FAST_TANH
     const float e = __builtin_amdgcn_exp2f(x * 2.88539008177792681f);  // 2 log2(e)
     return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
-#else
-    return tanhf(x);
-#endif
 }
 
-// two at a time (FENV_PPO_TANH_PK): the same operations as float2, so the multiply / add /
+// two at a time: the same operations as float2, so the multiply / add /
 // fma steps issue as packed fp32
-#ifndef FENV_PPO_TANH_PK
-#define FENV_PPO_TANH_PK 1
-#endif
 // (An accurate small-argument tanh -- an odd polynomial below |x| = 0.55, where the exp form
 // loses up to 1.4e-3 relative, 1.6e-7 absolute -- costs 0.5 us per minibatch and lands no closer to
 // torch at the reference config, measured in rounds 3 and 4: profiles/ab/r3_ppo_tanh_ab.txt,
 // profiles/ab/r4_ppo_precision_ab.txt; source at commit 2c54623.)
 __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1) {
-#if FENV_PPO_FAST_TANH && FENV_PPO_TANH_PK
     using f2 = float __attribute__((ext_vector_type(2)));
     const f2 x = {x0, x1};
     const f2 t = x * 2.88539008177792681f;  // 2 log2(e)
@@ -180,22 +169,14 @@ __device__ __forceinline__ void tanh_u2(float x0, float x1, float &y0, float &y1
     const f2 y = 1.0f - 2.0f * r;
     y0 = y.x;
     y1 = y.y;
-#else
-    y0 = tanh_u(x0);
-    y1 = tanh_u(x1);
-#endif
 }
 
 #ifndef FENV_PPO_UDZ
 #define FENV_PPO_UDZ 4  // unroll of the dL/dz2 loop (16 steps)
 #endif
-#ifndef FENV_PPO_BSUM4
-#define FENV_PPO_BSUM4 1  // bias-gradient column sums over all kPB rows in 4 partial sums (0: B rows, one chain)
-#endif
 // Column sum of an activation-gradient image (rows at stride kRow): the bias gradient.  Rows
 // b >= B of dL/dz2 and dL/dz1 are exact zeros, so summing all kPB rows adds only zeros.
 __device__ __forceinline__ float col_sum(const float *z, int B) {
-#if FENV_PPO_BSUM4
     (void)B;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
@@ -206,22 +187,12 @@ __device__ __forceinline__ float col_sum(const float *z, int B) {
         a3 += z[(b + 3) * kRow];
     }
     return (a0 + a1) + (a2 + a3);
-#else
-    float acc = 0.f;
-#pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += z[b * kRow];
-    return acc;
-#endif
 }
 
-// Sum over the 64 lanes, in every lane.  FENV_PPO_DPP_SUM (default): DPP row shifts and row
+// Sum over the 64 lanes, in every lane: DPP row shifts and row
 // broadcasts (a fixed order; six VALU ops and one v_readlane) instead of six dependent
 // ds_bpermute round trips of the xor butterfly.
-#ifndef FENV_PPO_DPP_SUM
-#define FENV_PPO_DPP_SUM 1
-#endif
 __device__ __forceinline__ float wsum(float v) {
-#if FENV_PPO_DPP_SUM
     int x = __float_as_int(v);
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false)));
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false)));
@@ -230,11 +201,6 @@ __device__ __forceinline__ float wsum(float v) {
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false)));
     x = __float_as_int(__int_as_float(x) + __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false)));
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
-#else
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
-#endif
 }
 
 // unroll of the two 32-step fp32 MFMA loops (layer-2 forward; W2 grads + dL/dh1)
@@ -243,12 +209,6 @@ __device__ __forceinline__ float wsum(float v) {
 #endif
 #ifndef FENV_PPO_U2
 #define FENV_PPO_U2 4
-#endif
-#ifndef FENV_PPO_RING
-#define FENV_PPO_RING 8  // > 0: W2-grad loop with an explicit operand ring of this depth
-#endif
-#ifndef FENV_PPO_RING_L2
-#define FENV_PPO_RING_L2 8  // > 0: the same for the layer-2 forward loop
 #endif
 // ring depths of the split launch (one wave per SIMD: a 512-register budget)
 #ifndef FENV_PPO_RING_SPLIT
@@ -457,10 +417,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #ifndef FENV_PPO_ADAM_PK
 #define FENV_PPO_ADAM_PK 1
 #endif
-#ifndef FENV_PPO_ADAM_FMA
-#define FENV_PPO_ADAM_FMA 1
-#endif
-    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && FENV_PPO_ADAM_FMA && KP % 2 == 0;
+    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && KP % 2 == 0;
     // ceil((64 D + 64) / 256) <= 3 for D <= 8 (4 when packed: slot pairs)
     constexpr int kKA = kAS ? (kPK ? 4 : 3) : KP;
     // dL/dz1 in the other network's H1 half (FENV_PPO_DZ1_SEP, split launch: each block owns
@@ -497,25 +454,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #define FENV_PPO_DZ1_PRE 1
 #endif
     constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
-#ifndef FENV_PPO_COEF_FAST
-#define FENV_PPO_COEF_FAST 1
-#endif
-#ifndef FENV_PPO_LC_FAST
-#define FENV_PPO_LC_FAST 1
-#endif
 #ifndef FENV_PPO_BC_WAVE
 #define FENV_PPO_BC_WAVE 1
 #endif
     constexpr bool kBCW = SPLIT && !GRAD && FENV_PPO_BC_WAVE;
     constexpr int kBC = 60;  // R slots: this minibatch's Adam step size and 1 / sqrt(bc2)
-#ifndef FENV_PPO_HG_VEC
-#define FENV_PPO_HG_VEC 1
-#endif
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
-    // Adam with the clip coefficient (fused form: FENV_PPO_ADAM_FMA)
-#ifndef FENV_PPO_ADAM_FMA
-#define FENV_PPO_ADAM_FMA 1
-#endif
+    // Adam with the clip coefficient (fused form)
     float a_coef = 0.f, a_ss = 0.f, a_ib = 0.f;  // clip coef, step size, 1/sqrt(bc2)
     float gq[SPLIT ? KP : 1], wq[SPLIT ? KP : 1];
     auto adam_slot = [&](int q) {
@@ -523,20 +468,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
         if (p < P) {
             const int ix = SPLIT ? lp[q] : lx(p);
             const float gr = (SPLIT ? gq[q] : G[ix]) * a_coef;
-#if FENV_PPO_ADAM_FMA
             m[q] = __builtin_fmaf(ar1, gr - m[q], m[q]);
             v[q] = __builtin_fmaf(ar2, gr * gr, v[q] * hp.beta2);
             const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v[q]), a_ib, hp.eps);
             const float wn = __builtin_fmaf(-a_ss, m[q] * __builtin_amdgcn_rcpf(den),
                                             SPLIT ? wq[q] : W[ix]);
-#else
-            m[q] = m[q] + ar1 * (gr - m[q]);
-            v[q] = v[q] * hp.beta2 + ar2 * (gr * gr);
-            // torch: denom = sqrt(v) / sqrt(bc2) + eps; p -= step_size * m / denom (here
-            // with v_sqrt_f32 and v_rcp_f32, each within 1 ulp)
-            const float den = __builtin_amdgcn_sqrtf(v[q]) * a_ib + hp.eps;
-            const float wn = (SPLIT ? wq[q] : W[ix]) - a_ss * (m[q] * __builtin_amdgcn_rcpf(den));
-#endif
             W[ix] = wn;
         }
     };
@@ -650,7 +586,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
             auto loss_consts = [&]() {
                 const float ls0 = W[lx(L.logstd)], ls1 = W[lx(L.logstd + 1)];
-#if FENV_PPO_LC_FAST
                 // the loss wave's chain starts from these: hardware exp / log / reciprocal
                 // (v_exp_f32, v_log_f32, v_rcp_f32: ~1 ulp) instead of libm expf / logf and
                 // correctly rounded divisions (~70 dependent instructions)
@@ -665,17 +600,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 lc_iv1 = __builtin_amdgcn_rcpf(lc_var1);
                 lc_i2v0 = 0.5f * lc_iv0;
                 lc_i2v1 = 0.5f * lc_iv1;
-#else
-                const float sd0 = expf(ls0), sd1 = expf(ls1);
-                lc_var0 = sd0 * sd0;
-                lc_var1 = sd1 * sd1;
-                lc_lsd0 = logf(sd0);  // torch: std.log()
-                lc_lsd1 = logf(sd1);
-                lc_i2v0 = 1.0f / (2.0f * lc_var0);
-                lc_i2v1 = 1.0f / (2.0f * lc_var1);
-                lc_iv0 = 1.0f / lc_var0;
-                lc_iv1 = 1.0f / lc_var1;
-#endif
             };
             // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
             // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
@@ -689,8 +613,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
-#if FENV_PPO_RING_L2
-                constexpr int RL = SPLIT ? FENV_PPO_RING_L2_SPLIT : FENV_PPO_RING_L2;
+                constexpr int RL = SPLIT ? FENV_PPO_RING_L2_SPLIT : 8;  // unsplit: ring depth 8
                 float ra[RL], rb[RL];
 #pragma unroll
                 for (int j = 0; j < RL; ++j) {
@@ -708,11 +631,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         }
                     }
                 }
-#else
-#pragma unroll FENV_PPO_UL2
-                for (int i = 0; i < 32; ++i)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ar[i], Bc[i], acc, 0, 0, 0);
-#endif
                 float *Hr = H2 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
                 for (int r = 0; r < 16; r += 2) {
@@ -971,12 +889,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *sg = S + (net ? sGV : sGMU0 + (c & 1)) * kPB;
                 const float *s0p = S + (net ? sGV : sGMU0) * kPB, *s1p = S + sGMU1 * kPB;
                 float ha[16], sb[16], s0[16], s1[16];
-                // sample of K-step t: b = 16 q + t (FENV_PPO_HG_VEC: the per-sample scalars of a
+                // sample of K-step t: b = 16 q + t (the per-sample scalars of a
                 // lane group are then 16 contiguous floats, read as four ds_read_b128) or 4 t + q
-                auto bidx = [&](int t) { return FENV_PPO_HG_VEC ? 16 * q + t : 4 * t + q; };
+                auto bidx = [&](int t) { return 16 * q + t; };
 #pragma unroll
                 for (int t = 0; t < 16; ++t) ha[t] = hcol[bidx(t) * kRow + c];
-#if FENV_PPO_HG_VEC
                 {
                     const float4 *g4 = reinterpret_cast<const float4 *>(sg + 16 * q);
                     const float4 *a4 = reinterpret_cast<const float4 *>(s0p + 16 * q);
@@ -990,15 +907,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         s1[4 * j] = z.x; s1[4 * j + 1] = z.y; s1[4 * j + 2] = z.z; s1[4 * j + 3] = z.w;
                     }
                 }
-#else
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int b = bidx(t);
-                    sb[t] = sg[b];
-                    s0[t] = s0p[b];
-                    s1[t] = net ? 0.0f : s1p[b];
-                }
-#endif
                 const int k = 16 * kt + c;
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
                 const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
@@ -1106,9 +1014,8 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         omh[r] = 1.0f - hv * hv;
                     }
                 }
-#if FENV_PPO_RING
                 // operands of step i + RD loaded while steps i.. issue (RD-deep register ring)
-                constexpr int RD = SPLIT ? FENV_PPO_RING_SPLIT : FENV_PPO_RING;
+                constexpr int RD = SPLIT ? FENV_PPO_RING_SPLIT : 8;  // unsplit: ring depth 8
                 const float *pa = Z2 + (32 * h) * kRow + 32 * mt + c;
                 const float *pb = A1 + (32 * h) * kRow + 32 * nt + c;
                 const float *pc = Z2 + (32 * mt + c) * kRow + 32 * h;
@@ -1136,17 +1043,6 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         }
                     }
                 }
-#else
-#pragma unroll FENV_PPO_U2
-                for (int i = 0; i < 32; ++i) {
-                    const int kk = 32 * h + i;
-                    gw = __builtin_amdgcn_mfma_f32_32x32x2f32(Z2[kk * kRow + 32 * mt + c],
-                                                             A1[kk * kRow + 32 * nt + c], gw, 0, 0, 0);
-                    dz = __builtin_amdgcn_mfma_f32_32x32x2f32(Z2[(32 * mt + c) * kRow + kk],
-                                                             W[w2 + kk * kRow + 32 * nt + c], dz,
-                                                             0, 0, 0);
-                }
-#endif
                 float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -1318,15 +1214,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 tot = R[32];
             }
             FENV_PPO_PHASE(9);
-            // FENV_PPO_COEF_FAST: v_sqrt_f32 and v_rcp_f32 (1 ulp each) instead of the correctly
+            // v_sqrt_f32 and v_rcp_f32 (1 ulp each) instead of the correctly
             // rounded square root and division (~25 dependent instructions after the exchange)
-#if FENV_PPO_COEF_FAST
             const float norm = __builtin_amdgcn_sqrtf(tot);
             float coef = hp.max_grad_norm * __builtin_amdgcn_rcpf(norm + 1e-6f);
-#else
-            const float norm = __builtin_sqrtf(tot);
-            float coef = hp.max_grad_norm / (norm + 1e-6f);
-#endif
             coef = coef < 1.0f ? coef : 1.0f;
             // ---- Adam (torch semantics: lerp first moment, bias-corrected step)
             a_coef = coef;
