@@ -420,11 +420,13 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
         m.collector.collect()
     m.train()  # warm-up (allocates the Adam state)
     torch.cuda.synchronize()
-    el = 0.0
+    el, col = 0.0, 0.0
     for _ in range(updates):
+        t0 = time.perf_counter()
         with torch.no_grad():
             m.collector.collect()
         torch.cuda.synchronize()
+        col += time.perf_counter() - t0
         t0 = time.perf_counter()
         m.train()
         torch.cuda.synchronize()
@@ -437,6 +439,10 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
                         f"10 epochs (SB3 defaults of the reference's PPO call)",
             "path": "fused" if m.use_fused else ("graph" if m.use_graph else "eager"),
             "ms_per_update": el / updates * 1e3, "us_per_minibatch": per_mb * 1e6,
+            # one whole training iteration (model.learn's loop body): rollout collection (fused
+            # policy + env kernel, GAE) + the update, in env agent-steps per second
+            "collect_ms": col / updates * 1e3,
+            "training_agent_steps_per_s": n / ((el + col) / updates),
             "samples_per_s": n * m.cfg.n_epochs / (el / updates),
             "gflops": flop / per_mb / 1e9,
             "exchange_reruns": m.exchange_retries,
