@@ -562,6 +562,14 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     return FENV_OK;
 }
 
+// Process exit with envs never destroyed: a draw-ahead thread may still be writing its host
+// slot while the HIP runtime tears down the pinned allocations.  This library's destructor runs
+// before the runtime's (it depends on it) and joins every live handle's thread first.
+__attribute__((destructor)) static void join_draws_at_exit() {
+    std::lock_guard<std::mutex> lk(live().mu);
+    for (const void *h : live().set) const_cast<fenv *>(static_cast<const fenv *>(h))->join_ahead();
+}
+
 int fenv_destroy(fenv_t *e) {
     if (!e) return FENV_OK;
     if (!live_take(e)) return fail(FENV_EINVAL, "fenv_destroy: not a live handle (destroyed twice?)");

@@ -6,6 +6,7 @@ cycle with their formation views, so every dropped env -- its device state, its 
 mirrors, its torch buffers -- was torn down by the cyclic collector at arbitrary points.  These
 tests churn a few hundred envs over every kernel path with explicit collections in between."""
 import gc
+import os
 import weakref
 
 import numpy as np
@@ -335,3 +336,26 @@ def test_mt_draw_ahead_across_events_and_release(venv, flib):
     env, bad = _mt_run(venv, 200_000, 5, 32, (6, 1, 4), streams=True)
     assert bad is None, bad
     env.release()
+
+
+def test_exit_with_a_draw_in_flight(tmp_path):
+    """A process that exits right after creating a large MT19937 env (its next reset set being
+    drawn on the host thread) and never releases it: the library joins the thread at unload,
+    before the HIP runtime frees the pinned slot it writes, so the process exits cleanly."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import torch, pkgload\n"
+            "pkg = pkgload.load()\n"
+            "from importlib import import_module\n"
+            "ve = import_module(pkg.__name__ + '.vectorized_env')\n"
+            "env = ve.FormationEnv({'num_formation': 400000, 'num_agents_per_formation': 5,\n"
+            "                       'goal_in_obs': True}, device='cuda:0', seed=3)\n"
+            "env.reset_tensor()\n"
+            "torch.cuda.synchronize()\n"
+            "import os; os._exit(0) if len(sys.argv) > 1 else None\n") % root
+    for args in ([], ["hard"]):
+        r = subprocess.run([sys.executable, "-c", code] + args, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, (args, r.returncode, r.stderr[-2000:])
