@@ -14,11 +14,14 @@
 // form of the same code.  Here the parameters,
 // their gradients and the minibatch's activations live in LDS (152 KB), each thread keeps the
 // Adam moments of the ~19 parameters it owns in registers, and the loop runs every minibatch of
-// every epoch inside one launch.  The 64-deep contractions (layer 2 forward, W2 gradients,
-// dL/dh1, W1 gradients) run on the fp32 MFMA pipe (v_mfma_f32_32x32x2f32 / 16x16x4f32: exact
-// fp32 products, fp32 accumulation); the parameter and gradient images are padded (lx) so the
-// operand reads are bank-conflict free, and the two 32-step MFMA loops keep the LDS reads of
-// step i + 8 in flight under the MFMAs of step i (an explicit register ring).  tanh is
+// every epoch inside one launch.  The 64-deep contractions run on the MFMA pipe: layer 2, W2
+// gradients and dL/dh1 (the three 32 x 32 x 64 tiles per wave) in split-f16 form -- x = hi + lo,
+// hi = x's leading 11 bits, lo = the remainder rounded to f16, three v_mfma_f32_32x32x16_f16
+// (hi*lo, lo*hi, hi*hi) per 16-deep chunk, exact products and fp32 accumulation, the dropped
+// lo*lo and lo's rounding < 2^-21 relative; dL/dz2 scaled by a power of two into f16's range
+// first, exactly undone -- and layer 1, the heads and W1 gradients on fp32
+// v_mfma_f32_16x16x4f32; the parameter and gradient images are padded (lx) so the operand reads
+// are bank-conflict free.  tanh is
 // 1 - 2 / (1 + e^2x) on v_exp/v_rcp and the gradient norm is summed by the threads that write
 // the gradient entries.  Results match the torch path to summation-order rounding plus the
 // tanh's < 3e-7 (tests/test_gpu_rollout.py).
@@ -88,6 +91,7 @@ static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
 enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV, sMU0, sMU1, sVAL,
        sPL, sCF, sGL0, sGL1, sVLS };  // the last five: per-sample loss terms (FENV_PPO_LOSS_SPREAD)
 constexpr int kEnt = 56;              // R slot: the entropy (FENV_PPO_LOSS_SPREAD)
+constexpr int kZM = 40;               // R slots [kZM, kZM + 8): per-wave max |dL/dz2| (wave w)
 
 struct PPOArgs {
     float *params, *exp_avg, *exp_avg_sq, *step;
@@ -601,9 +605,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 lc_i2v0 = 0.5f * lc_iv0;
                 lc_i2v1 = 0.5f * lc_iv1;
             };
-            // ---- layer 2 on v_mfma_f32_32x32x2f32: wave w = one 32 x 32 tile (net w>>2, sample
-            // rows 32((w>>1)&1), hidden cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as 32 MFMAs
-            // (slot h of lane half h carries k = 32h + i).  Every row runs (rows >= B are unused).
+            // ---- layer 2: wave w = one 32 x 32 tile (net w>>2, sample rows 32((w>>1)&1), hidden
+            // cols 32(w&1)) of Z2 = b2 + H1 . W2^T, K = 64 as four 16-deep split-f16 chunks
+            // (12 v_mfma_f32_32x32x16_f16 instead of 32 fp32 32x32x2: round 4, 8.60-8.74 ->
+            // 8.21-8.29 us per minibatch with this phase alone).  Every row runs (rows >= B unused).
             {
                 const int net = w >> 2, mt = (w >> 1) & 1, nt = w & 1, h = lane >> 5;
                 const int c = lane & 31;
@@ -613,23 +618,23 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = bias;
-                constexpr int RL = SPLIT ? FENV_PPO_RING_L2_SPLIT : 8;  // unsplit: ring depth 8
-                float ra[RL], rb[RL];
+                // lane half h carries k = 32h + 8cc + j of chunk cc; small terms first
+                float av[4][8], bv[4][8];
 #pragma unroll
-                for (int j = 0; j < RL; ++j) {
-                    ra[j] = Ar[j];
-                    rb[j] = Bc[j];
-                }
+                for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
-                for (int i0 = 0; i0 < 32; i0 += RL) {
-#pragma unroll
-                    for (int j = 0; j < RL; ++j) {
-                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], acc, 0, 0, 0);
-                        if (i0 + RL + j < 32) {
-                            ra[j] = Ar[i0 + RL + j];
-                            rb[j] = Bc[i0 + RL + j];
-                        }
+                    for (int j = 0; j < 8; ++j) {
+                        av[cc][j] = Ar[8 * cc + j];
+                        bv[cc][j] = Bc[8 * cc + j];
                     }
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    h8 ah, al, bh, bl;
+                    split8(av[cc], 0, ah, al);
+                    split8(bv[cc], 0, bh, bl);
+                    acc = mma16(ah, bl, acc);
+                    acc = mma16(al, bh, acc);
+                    acc = mma16(ah, bh, acc);
                 }
                 float *Hr = H2 + (net * kPB + 32 * mt) * kRow + 32 * nt + c;
 #pragma unroll
@@ -924,6 +929,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc[r] += acc2[r];
                 float b2p = 0.0f;  // kB2: this lane's part of the b2 gradient of column k
+                float zmx = 0.0f;  // max |dL/dz2| of the lane's entries (split-f16 W2 phase scale)
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const int b = bidx(t);
@@ -933,7 +939,11 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     const float dzb = b < B ? dz : 0.0f;
                     hcol[b * kRow + c] = dzb;
                     if (kB2) b2p += dzb;
+                    zmx = fmaxf(zmx, fabsf(dzb));
                 }
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) zmx = fmaxf(zmx, __shfl_xor(zmx, m, 64));
+                if (lane == 0) R[kZM + w] = zmx;
                 if constexpr (kB2) {  // b2 gradient = column sum of dL/dz2 (the 4 lane groups)
                     b2p += __shfl_xor(b2p, 16, 64);
                     b2p += __shfl_xor(b2p, 32, 64);
@@ -973,6 +983,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int k = 16 * kt + c;
                 const float wa0 = W[lx((net ? L.valW : L.actW) + k)];
                 const float wa1 = net ? 0.0f : W[lx(L.actW + kHid + k)];
+                float zmx = 0.0f;
 #pragma unroll FENV_PPO_UDZ
                 for (int t = 0; t < 16; ++t) {
                     const int b = 4 * t + q;
@@ -985,13 +996,18 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         v = gh * (1.0f - hv * hv);
                     }
                     *hp2 = v;
+                    zmx = fmaxf(zmx, fabsf(v));
                 }
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) zmx = fmaxf(zmx, __shfl_xor(zmx, m, 64));
+                if (lane == 0) R[kZM + w] = zmx;
             }
             __syncthreads();
             FENV_PPO_PHASE(4);
             FENV_PPO_PHASE(5);
-            // ---- W2 gradients GW2 = dZ2^T . H1 and dL/dh1 = dZ2 . W2, both on
-            // v_mfma_f32_32x32x2f32 with K = 64 (samples b resp. hidden j; slot h <-> 32h + i).
+            // ---- W2 gradients GW2 = dZ2^T . H1 and dL/dh1 = dZ2 . W2, both with K = 64 (samples b
+            // resp. hidden j) as four 16-deep split-f16 chunks (round 4: 24 v_mfma_f32_32x32x16_f16
+            // instead of 64 fp32 32x32x2; with layer 2, 8.60-8.74 -> 7.79-7.96 us per minibatch).
             // Wave w owns tile (net w>>2, rows 32((w>>1)&1), cols 32(w&1)) of each; dL/dz1
             // overwrites H1 only after the barrier (GW2 reads H1).
             {
@@ -1014,34 +1030,46 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                         omh[r] = 1.0f - hv * hv;
                     }
                 }
-                // operands of step i + RD loaded while steps i.. issue (RD-deep register ring)
-                constexpr int RD = SPLIT ? FENV_PPO_RING_SPLIT : 8;  // unsplit: ring depth 8
+                // split-f16 chains (three v_mfma_f32_32x32x16_f16 per 16-deep chunk, lane half h
+                // carrying k = 32h + 8cc + j); dL/dz2 scaled by a power of two so its largest
+                // entry sits at 2^10..2^11 in f16 (exact: the results are scaled back)
+                const float *zmw = R + kZM + 4 * net;  // this network's four wave maxima
+                const float zm = fmaxf(fmaxf(zmw[0], zmw[1]), fmaxf(zmw[2], zmw[3]));
+                int se = 264 - (int)((__float_as_uint(zm) >> 23) & 0xFFu);  // 127 + 10 - e
+                se = se < 1 ? 1 : (se > 254 ? 254 : se);
+                const float zs = __uint_as_float((uint32_t)se << 23);
+                const float zi = __uint_as_float((uint32_t)(254 - se) << 23);
                 const float *pa = Z2 + (32 * h) * kRow + 32 * mt + c;
                 const float *pb = A1 + (32 * h) * kRow + 32 * nt + c;
                 const float *pc = Z2 + (32 * mt + c) * kRow + 32 * h;
                 const float *pd = W + w2 + (32 * h) * kRow + 32 * nt + c;
-                float ra[RD], rb[RD], rc[RD], rd[RD];
 #pragma unroll
-                for (int j = 0; j < RD; ++j) {
-                    ra[j] = pa[j * kRow];
-                    rb[j] = pb[j * kRow];
-                    rc[j] = pc[j];
-                    rd[j] = pd[j * kRow];
+                for (int cc = 0; cc < 4; ++cc) {
+                    float va[8], vb[8], vc[8], vd[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int i = 8 * cc + j;
+                        va[j] = pa[i * kRow] * zs;
+                        vb[j] = pb[i * kRow];
+                        vc[j] = pc[i] * zs;
+                        vd[j] = pd[i * kRow];
+                    }
+                    h8 ah, al, bh, bl, ch, cl, dh, dl;
+                    split8(va, 0, ah, al);
+                    split8(vb, 0, bh, bl);
+                    split8(vc, 0, ch, cl);
+                    split8(vd, 0, dh, dl);
+                    gw = mma16(ah, bl, gw);
+                    dz = mma16(ch, dl, dz);
+                    gw = mma16(al, bh, gw);
+                    dz = mma16(cl, dh, dz);
+                    gw = mma16(ah, bh, gw);
+                    dz = mma16(ch, dh, dz);
                 }
 #pragma unroll
-                for (int i0 = 0; i0 < 32; i0 += RD) {
-#pragma unroll
-                    for (int j = 0; j < RD; ++j) {
-                        gw = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[j], rb[j], gw, 0, 0, 0);
-                        dz = __builtin_amdgcn_mfma_f32_32x32x2f32(rc[j], rd[j], dz, 0, 0, 0);
-                        const int i = i0 + RD + j;
-                        if (i < 32) {
-                            ra[j] = pa[i * kRow];
-                            rb[j] = pb[i * kRow];
-                            rc[j] = pc[i];
-                            rd[j] = pd[i * kRow];
-                        }
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    gw[r] *= zi;
+                    dz[r] *= zi;
                 }
                 float *Gr = G + w2 + 32 * mt * kRow + 32 * nt + c;
 #pragma unroll
