@@ -207,20 +207,19 @@ __device__ __forceinline__ float wsum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
 
-// unroll of the two 32-step fp32 MFMA loops (layer-2 forward; W2 grads + dL/dh1)
-#ifndef FENV_PPO_UL2
-#define FENV_PPO_UL2 8
-#endif
-#ifndef FENV_PPO_U2
-#define FENV_PPO_U2 4
-#endif
-// ring depths of the split launch (one wave per SIMD: a 512-register budget)
-#ifndef FENV_PPO_RING_SPLIT
-#define FENV_PPO_RING_SPLIT 32
-#endif
-#ifndef FENV_PPO_RING_L2_SPLIT
-#define FENV_PPO_RING_L2_SPLIT 32
-#endif
+// Max over the 64 lanes of non-negative values (same DPP pattern as wsum: lanes shifted in
+// from outside a row read 0, the identity here), wave-uniform.
+__device__ __forceinline__ float wmax_nn(float v) {
+    int x = __float_as_int(v);
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false))));
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
 #ifndef FENV_PPO_DUMP_GRAD
 #define FENV_PPO_DUMP_GRAD 0
 #endif
@@ -941,8 +940,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     if (kB2) b2p += dzb;
                     zmx = fmaxf(zmx, fabsf(dzb));
                 }
-#pragma unroll
-                for (int m = 32; m >= 1; m >>= 1) zmx = fmaxf(zmx, __shfl_xor(zmx, m, 64));
+                zmx = wmax_nn(zmx);
                 if (lane == 0) R[kZM + w] = zmx;
                 if constexpr (kB2) {  // b2 gradient = column sum of dL/dz2 (the 4 lane groups)
                     b2p += __shfl_xor(b2p, 16, 64);
@@ -998,8 +996,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     *hp2 = v;
                     zmx = fmaxf(zmx, fabsf(v));
                 }
-#pragma unroll
-                for (int m = 32; m >= 1; m >>= 1) zmx = fmaxf(zmx, __shfl_xor(zmx, m, 64));
+                zmx = wmax_nn(zmx);
                 if (lane == 0) R[kZM + w] = zmx;
             }
             __syncthreads();
