@@ -453,16 +453,19 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
 
 def ppo_pmc_mfma():
     """Counter-backed MFMA-pipe occupancy of k_ppo_update from the committed PMC passes
-    (tools/ppo_pmc.sh -> profiles/r3_ppo_pmc_sq.json; not measured in this run).  The kernel runs
-    8 waves on 8 SIMDs (4 per CU, actor and critic CU); SQ_VALU_MFMA_BUSY_CYCLES counts cycles
-    summed over the chip, GRBM_GUI_ACTIVE the kernel's cycles summed over the 8 XCDs."""
-    p = os.path.join(ROOT, "profiles", "r3_ppo_pmc_sq.json")
+    (tools/job_r4_ppopmc.sh -> profiles/r4_ppo_pmc_sq.json, else round 3's; not measured in this
+    run).  The kernel runs 8 waves on 8 SIMDs (4 per CU, actor and critic CU);
+    SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over the chip, GRBM_GUI_ACTIVE the kernel's
+    cycles summed over the 8 XCDs."""
+    p = os.path.join(ROOT, "profiles", "r4_ppo_pmc_sq.json")
+    if not os.path.exists(p):
+        p = os.path.join(ROOT, "profiles", "r3_ppo_pmc_sq.json")
     try:
         k = next(iter(json.load(open(p))["kernels"].values()))
         cycles = k["GRBM_GUI_ACTIVE"] / 8.0
         return {"busy_frac": k["SQ_VALU_MFMA_BUSY_CYCLES"] / 8.0 / cycles,
                 "mfma_per_dispatch": k["SQ_INSTS_MFMA"], "kernel_cycles": cycles,
-                "pmc_source": "profiles/r3_ppo_pmc_sq.json"}
+                "pmc_source": os.path.relpath(p, ROOT)}
     except Exception as ex:  # noqa: BLE001
         return {"error": f"{type(ex).__name__}: {ex}"}
 
