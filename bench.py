@@ -723,7 +723,10 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
-                       "episode_phase": phase, "timed_launches": plan,
+                       "episode_phase": phase,
+                       # steps per timed launch: {count, steps} when uniform, else the list
+                       "timed_launches": ({"count": len(plan), "steps": plan[0]}
+                                          if plan and len(set(plan)) == 1 else plan),
                        "parallelism": f"formation-shard dp{world} ({scaling}: "
                                        + ("formations split over the ranks"
                                           if scaling == "strong" else
