@@ -584,7 +584,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(1);
-            // the loss's log_std-derived constants (computed by the loss wave)
+            // the loss's log_std-derived constants (formed by every wave in the heads phase)
             float lc_var0 = 0.f, lc_var1 = 0.f, lc_lsd0 = 0.f, lc_lsd1 = 0.f;
             float lc_i2v0 = 0.f, lc_i2v1 = 0.f, lc_iv0 = 0.f, lc_iv1 = 0.f;
             auto loss_consts = [&]() {
@@ -648,6 +648,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             // ---- heads mu = actW . h2_pi + actb, value = valW . h2_vf + valb on
             // v_mfma_f32_16x16x4f32: wave w = net w>>2, samples 16(w&3)..+15, output columns 0..15
             // of which 2 (actor) / 1 (critic) are real; K = 64 hidden as 16 MFMAs
+            // The loss constants are formed here, in this phase's MFMA shadow (every wave), off the
+            // loss wave's dependent chain (round 4, with the hardware-exp ratio and the late loss
+            // sums: 7.83 -> 7.72 us per minibatch, profiles/ab/r4_ppo_loss_phase_ab.txt)
+            loss_consts();
             {
                 const int net = w >> 2, bt = w & 3, q = lane >> 4, c = lane & 15;
                 const int ncol = net ? 1 : 2;
@@ -698,14 +702,13 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if (wl == 0) {
                 const bool do_pi = !SPLIT || net_b == 0, do_vf = !SPLIT || net_b == 1;
                 const bool on = lane < B;
-                if (!kSpread || do_pi) loss_consts();
                 const float lsd0 = lc_lsd0, lsd1 = lc_lsd1, i2v0 = lc_i2v0, i2v1 = lc_i2v1;
                 const float iv0 = lc_iv0, iv1 = lc_iv1;
                 float pl = 0.f, vl = 0.f, cf = 0.f, gls0 = 0.f, gls1 = 0.f, gmu0 = 0.f, gmu1 = 0.f;
                 float gv = 0.f;
                 if constexpr (kSpread) {
                     // split launch: this block's terms only; the sums over the samples are taken
-                    // by waves 1-3 at the start of the next phase (per-sample values in S)
+                    // after the barrier (loss_sums, loss_stats; per-sample values in S)
                     const float kLogSqrt2Pi = 0.918938533204672742f;
                     if (do_pi) {
                         if (on) {
@@ -714,7 +717,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                             const float d0 = a0 - mu0, d1 = a1 - mu1;
                             const float lp = (-(d0 * d0) * i2v0 - lsd0 - kLogSqrt2Pi) +
                                              (-(d1 * d1) * i2v1 - lsd1 - kLogSqrt2Pi);
-                            const float ratio = expf(lp - S[sOLP * kPB + lane]);
+                            // v_exp_f32 on a log2(e) product (~2 ulp for the |log ratio| < 1 that
+                            // stays unclipped) instead of libm expf's range-reduced form
+                            const float ratio = __builtin_amdgcn_exp2f(
+                                (lp - S[sOLP * kPB + lane]) * 1.44269504088896341f);
                             const float an = S[sADV * kPB + lane];
                             const float lo = 1.0f - hp.clip_range, hi = 1.0f + hp.clip_range;
                             const float rc = ratio < lo ? lo : (ratio > hi ? hi : ratio);
@@ -834,46 +840,45 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             }
             __syncthreads();
             FENV_PPO_PHASE(3);
-            // kSpread: the loss sums, one or two per wave of waves 1-3 (wave 0 just ran the loss);
-            // their outputs are only read from the norm phase on
-            auto loss_sums = [&]() {
-                if (net_b == 0) {
-                    if (wl == 1) {
+            // kSpread: the loss sums.  The four actor gradient sums go one per wave (waves 0-3,
+            // branch-free; the critic's value-bias sum to wave 2); the statistics sums (policy /
+            // value loss, clip fraction) wait for the norm phase's exchange shadow (loss_stats),
+            // except in gradient mode, which has no norm phase.  Their outputs are only read from
+            // the norm phase on.
+            auto loss_stats = [&]() {
+                if (wl == 1) {
+                    if (net_b == 0) {
                         const float spl = wsum(S[sPL * kPB + lane]), scf = wsum(S[sCF * kPB + lane]);
                         if (lane == 0) {
                             st_pl += (double)(-spl * invB);
                             if (!GRAD || g.ent_once) st_el += (double)(-R[kEnt]);
                             st_cf += (double)(scf * invB);
                         }
-                    } else if (wl == 2) {
-                        // d(ent_coef * entropy_loss)/d log_std_j = -ent_coef; gradient mode: the
-                        // entropy term once over the ranks (ent_once)
-                        const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
-                        const float g0 = wsum(S[sGL0 * kPB + lane]) - ec;
-                        const float g1 = wsum(S[sGL1 * kPB + lane]) - ec;
-                        if (lane == 0) {
-                            G[lx(L.logstd)] = g0;
-                            G[lx(L.logstd + 1)] = g1;
-                            gss += g0 * g0 + g1 * g1;
-                        }
-                    } else if (wl == 3) {
-                        const float m0 = wsum(S[sGMU0 * kPB + lane]), m1 = wsum(S[sGMU1 * kPB + lane]);
-                        if (lane == 0) {
-                            G[lx(L.actb)] = m0;
-                            G[lx(L.actb + 1)] = m1;
-                            gss += m0 * m0 + m1 * m1;
-                        }
-                    }
-                } else {
-                    if (wl == 1) {
+                    } else {
                         const float svl = wsum(S[sVLS * kPB + lane]);
                         if (lane == 0) st_vl += (double)(svl * invB);
-                    } else if (wl == 2) {
-                        const float sgv = wsum(S[sGV * kPB + lane]);
-                        if (lane == 0) {
-                            G[lx(L.valb)] = sgv;
-                            gss += sgv * sgv;
-                        }
+                    }
+                }
+            };
+            auto loss_sums = [&]() {
+                if constexpr (GRAD) loss_stats();
+                if (net_b == 0) {
+                    // wave wl: d log_std_0, d log_std_1, d actb_0, d actb_1.  d(ent_coef *
+                    // entropy_loss)/d log_std_j = -ent_coef; gradient mode: the entropy term once
+                    // over the ranks (ent_once)
+                    const float ec = (!GRAD || g.ent_once) ? hp.ent_coef : 0.0f;
+                    const int slot = wl == 0 ? sGL0 : (wl == 1 ? sGL1 : (wl == 2 ? sGMU0 : sGMU1));
+                    const int gi = wl < 2 ? L.logstd + wl : L.actb + (wl - 2);
+                    const float v = wsum(S[slot * kPB + lane]) - (wl < 2 ? ec : 0.0f);
+                    if (lane == 0) {
+                        G[lx(gi)] = v;
+                        gss += v * v;
+                    }
+                } else if (wl == 2) {
+                    const float sgv = wsum(S[sGV * kPB + lane]);
+                    if (lane == 0) {
+                        G[lx(L.valb)] = sgv;
+                        gss += sgv * sgv;
                     }
                 }
             };
@@ -1208,6 +1213,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     }
                 }
                 if (FENV_PPO_POST_FIRST) read_gw();
+                if constexpr (kSpread && !GRAD) loss_stats();
                 // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
                 // at this minibatch's gather) while the first load is in flight
                 if (net_b == 0 && wl == 0 && kmb + 1 < nmb) {
