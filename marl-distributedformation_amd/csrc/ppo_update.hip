@@ -80,7 +80,7 @@ constexpr int oPH1 = oPO + kPB * 9;           // [2][kPB][kRow] layer-1 tanh, th
 constexpr int oPH2 = oPH1 + 2 * kPB * kRow;   // [2][kPB][kRow] layer-2 tanh, then dL/dz2
 constexpr int oPS = oPH2 + 2 * kPB * kRow;    // [16][kPB] per-sample scalars
 constexpr int oPR = oPS + 16 * kPB;           // [64] reduction scratch
-constexpr int oPB1 = oPR + 64;                // [2][64] b1-gradient partial sums (FENV_PPO_B1_PART)
+constexpr int oPB1 = oPR + 64;                // [2][64] b1-gradient partial sums (split launch)
 constexpr int kPPOLds = oPB1 + 2 * kHid;
 constexpr size_t kPPOLdsBytes = (size_t)kPPOLds * sizeof(float);
 static_assert(kPPOLdsBytes <= 160 * 1024, "fused PPO update exceeds the 160 KiB LDS of a CU");
@@ -89,8 +89,8 @@ static_assert(2 * (kHid * 9 + kHid * (kHid + 1)) + 3 * (kHid + 1) + 2 <= kMaxP,
 
 // per-sample scalar slots
 enum { sA0 = 0, sA1, sOLP, sADV, sRET, sGMU0, sGMU1, sGV, sMU0, sMU1, sVAL,
-       sPL, sCF, sGL0, sGL1, sVLS };  // the last five: per-sample loss terms (FENV_PPO_LOSS_SPREAD)
-constexpr int kEnt = 56;              // R slot: the entropy (FENV_PPO_LOSS_SPREAD)
+       sPL, sCF, sGL0, sGL1, sVLS };  // the last five: per-sample loss terms (split launch)
+constexpr int kEnt = 56;              // R slot: the entropy (split launch)
 constexpr int kZM = 40;               // R slots [kZM, kZM + 8): per-wave max |dL/dz2| (wave w)
 
 struct PPOArgs {
@@ -385,13 +385,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     int64_t e2 = 0, s2 = 0;  // position of minibatch kmb + 2
     advance(e2, s2);
     advance(e2, s2);
-    // Late gather (FENV_PPO_LATE_GATHER, split launch): the next minibatch's observations and
+    // Late gather (split launch): the next minibatch's observations and
     // per-sample inputs go to LDS at the END of a minibatch, after its last O / S read and
     // while thread 0 waits on the norm exchange, instead of at the start of the next one.
-#ifndef FENV_PPO_LATE_GATHER
-#define FENV_PPO_LATE_GATHER 1
-#endif
-    constexpr bool kLate = SPLIT && !GRAD && FENV_PPO_LATE_GATHER;
+    constexpr bool kLate = SPLIT && !GRAD;
     auto gather_store = [&](int Bk, float adv_val) {
 #pragma unroll
         for (int j = 0; j < OPT; ++j) {
@@ -408,59 +405,26 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
     };
     float adv_nx = 0.0f;
     if (SPLIT && net_b == 0 && wl == 0) adv_nx = adv_norm((int)(n < bs ? n : bs), ps[3]);
-    // Adam split (FENV_PPO_ADAM_SPLIT, split launch): a minibatch's Adam step updates the slots
+    // Adam split (split launch): a minibatch's Adam step updates the slots
     // holding layer 1 (W1, b1: slots 0..kKA-1 of every thread, PLayout puts them first) before
     // the barrier, and the other slots (W2, b2, heads, log_std) only in the next minibatch's
     // layer-1 phase, whose MFMAs and tanh never read them: the scheduler fills layer 1's
     // latencies with the register-only Adam arithmetic.  Same operations, same results.
-#ifndef FENV_PPO_ADAM_SPLIT
-#define FENV_PPO_ADAM_SPLIT 1
-#endif
-    constexpr bool kAS = SPLIT && !GRAD && FENV_PPO_ADAM_SPLIT;
-#ifndef FENV_PPO_ADAM_PK
-#define FENV_PPO_ADAM_PK 1
-#endif
-    constexpr bool kPK = SPLIT && FENV_PPO_ADAM_PK && KP % 2 == 0;
+    constexpr bool kAS = SPLIT && !GRAD;
+    constexpr bool kPK = SPLIT && KP % 2 == 0;
     // ceil((64 D + 64) / 256) <= 3 for D <= 8 (4 when packed: slot pairs)
     constexpr int kKA = kAS ? (kPK ? 4 : 3) : KP;
-    // dL/dz1 in the other network's H1 half (FENV_PPO_DZ1_SEP, split launch: each block owns
+    // dL/dz1 in the other network's H1 half (split launch: each block owns
     // the whole LDS image but runs one network, so that half is free)
-#ifndef FENV_PPO_DZ1_SEP
-#define FENV_PPO_DZ1_SEP 1
-#endif
-    constexpr bool kZ1S = SPLIT && FENV_PPO_DZ1_SEP && !FENV_PPO_DUMP_GRAD;
-#ifndef FENV_PPO_LOSS_SPREAD
-#define FENV_PPO_LOSS_SPREAD 1
-#endif
+    constexpr bool kZ1S = SPLIT && !FENV_PPO_DUMP_GRAD;
     // split launch: the loss wave writes per-sample terms; waves 1-3 take the sums afterwards
-    constexpr bool kSpread = SPLIT && FENV_PPO_LOSS_SPREAD;
+    constexpr bool kSpread = SPLIT;
     const int stat_tid = kSpread ? 64 : 0;  // the thread accumulating the loss statistics
-#ifndef FENV_PPO_B2_HG
-#define FENV_PPO_B2_HG 1  // split: the b2 gradient summed by the head-gradient phase's lanes
-#endif
-#ifndef FENV_PPO_B1_PART
-#define FENV_PPO_B1_PART 1  // split: b1-gradient partial sums from the dL/dz1 writers
-#endif
-    constexpr bool kB2 = SPLIT && FENV_PPO_B2_HG;
-    constexpr bool kB1 = SPLIT && FENV_PPO_B1_PART;
-#ifndef FENV_PPO_POST_FIRST
-#define FENV_PPO_POST_FIRST 1
-#endif
-#ifndef FENV_PPO_ACC2
-#define FENV_PPO_ACC2 1  // split: 16-step 16x16x4 MFMA chains as two interleaved accumulators
-#endif
-    constexpr bool kAcc2 = SPLIT && FENV_PPO_ACC2;
-#ifndef FENV_PPO_HEADS_K16
-#define FENV_PPO_HEADS_K16 1
-#endif
-#ifndef FENV_PPO_DZ1_PRE
-#define FENV_PPO_DZ1_PRE 1
-#endif
-    constexpr bool kDZP = SPLIT && FENV_PPO_DZ1_PRE;
-#ifndef FENV_PPO_BC_WAVE
-#define FENV_PPO_BC_WAVE 1
-#endif
-    constexpr bool kBCW = SPLIT && !GRAD && FENV_PPO_BC_WAVE;
+    constexpr bool kB2 = SPLIT;  // split: the b2 gradient summed by the head-gradient phase's lanes
+    constexpr bool kB1 = SPLIT;  // split: b1-gradient partial sums from the dL/dz1 writers
+    constexpr bool kAcc2 = SPLIT;  // split: 16-step 16x16x4 MFMA chains as two interleaved accumulators
+    constexpr bool kDZP = SPLIT;
+    constexpr bool kBCW = SPLIT && !GRAD;
     constexpr int kBC = 60;  // R slots: this minibatch's Adam step size and 1 / sqrt(bc2)
     const int zb = kZ1S ? (net_b ^ 1) : 0;  // H1 half holding dL/dz1 (unsplit: per network)
     // Adam with the clip coefficient (fused form)
@@ -479,7 +443,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             W[ix] = wn;
         }
     };
-    // Split launch, FENV_PPO_ADAM_PK: two slots per step as float2 arithmetic, so the compiler
+    // Split launch: two slots per step as float2 arithmetic, so the compiler
     // issues packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of fp32
     // per VALU slot); same operations and roundings as two adam_slot calls (fused form)
     using f2 = float __attribute__((ext_vector_type(2)));
@@ -659,12 +623,12 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const int hw = net ? L.valW : L.actW + (c & 1) * kHid;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                 if constexpr (SPLIT) {  // operands read up front, branch-free (see head grads)
-                    // K-step s4 of lane group q: hidden unit 16 q + s4 (FENV_PPO_HEADS_K16: the
-                    // 64 lanes of a read hit 64 banks) or 4 s4 + q
+                    // K-step s4 of lane group q: hidden unit 16 q + s4 (the 64 lanes of a read hit
+                    // 64 banks)
                     float av[16], wv[16];
 #pragma unroll
                     for (int s4 = 0; s4 < 16; ++s4) {
-                        const int kk = FENV_PPO_HEADS_K16 ? 16 * q + s4 : 4 * s4 + q;
+                        const int kk = 16 * q + s4;
                         av[s4] = a[kk - q];
                         wv[s4] = W[lx(hw + kk)];
                     }
@@ -1175,10 +1139,10 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
             if (lane == 0) R[wl] = gss;
             __syncthreads();
             FENV_PPO_PHASE(8);
-            // split: this thread's gradient and parameter entries are read now, so the LDS
-            // reads overlap the norm exchange below (FENV_PPO_POST_FIRST: after the post -- LDS
-            // reads complete in order, so 40 reads queued ahead of the partial's own would
-            // delay the post)
+            // split: this thread's gradient and parameter entries are read right after the post
+            // of the norm exchange below, so the LDS reads overlap its wait (not before it: LDS
+            // reads complete in order, so 40 reads queued ahead of the partial's own would delay
+            // the post)
             auto read_gw = [&]() {
                 if constexpr (SPLIT) {
 #pragma unroll
@@ -1188,8 +1152,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                     }
                 }
             };
-            if (!FENV_PPO_POST_FIRST) read_gw();
-            float tot = 0.f;
+                        float tot = 0.f;
             for (int q = 0; q < NT / 64; ++q) tot += R[q];
             if (SPLIT) {
                 // the other network's partial (actor's first in the sum on both blocks).  The
@@ -1212,7 +1175,7 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
-                if (FENV_PPO_POST_FIRST) read_gw();
+                read_gw();
                 if constexpr (kSpread && !GRAD) loss_stats();
                 // the actor's wave 0 normalises the next minibatch's advantages (loaded into ps
                 // at this minibatch's gather) while the first load is in flight
