@@ -20,25 +20,11 @@ __device__ __forceinline__ float norm2(float x, float y) {
     return __builtin_sqrtf(__builtin_fmaf(y, y, xx));
 }
 
-// x / Y (Y = 400 or 600), correctly rounded.  FENV_DIV_CONST=1: q0 = x*RN(1/Y) plus one fma
-// residual correction (3 dependent ops instead of the ~10 of the IEEE division sequence), which
-// equals IEEE x/Y for every finite |x| >= 2^-100 (tools/div_const_check.c, exhaustive); the
-// IEEE division is kept behind a branch for the rest (tiny, inf, NaN).  Default off (A/B'd per
-// config: profiles/ab/).
-#ifndef FENV_DIV_CONST
-#define FENV_DIV_CONST 0
-#endif
+// x / Y (Y = 400 or 600), correctly rounded: the IEEE division.  (A reciprocal-product form with
+// one fma residual correction, exact for every finite |x| >= 2^-100 by tools/div_const_check.c,
+// was A/B'd per config in rounds 1-2 and not kept: DESIGN.md section 4.)
 template <int Y>
 __device__ __forceinline__ float div_const(float x) {
-#if FENV_DIV_CONST
-    constexpr float y = (float)Y;
-    constexpr float c = 1.0f / (float)Y;
-    if (__builtin_expect(__builtin_fabsf(x) >= 0x1p-100f && __builtin_fabsf(x) <= 0x1p+127f, 1)) {
-        const float q0 = x * c;
-        const float r = __builtin_fmaf(-q0, y, x);
-        return __builtin_fmaf(r, c, q0);
-    }
-#endif
     return x / (float)Y;
 }
 
