@@ -556,26 +556,33 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     obs = torch.empty((T, A, D), dtype=torch.float32, device=dev)
     rew = torch.empty((T, A), dtype=torch.float32, device=dev)
     done = torch.empty((T, A), dtype=torch.bool, device=dev)
-    # stats pipeline: a stats launch writes partials[s] on the main stream; a side stream reduces
-    # them (deterministic order) and all-reduces the two doubles over RCCL, overlapped with the
-    # next launches; the launch after next that reuses partials[s] waits for the side stream.
+    # Stats pipeline: a stats launch writes its per-wave {reward, done} records into partials[s]
+    # on the main stream and records mark[s]; once the NEXT launch has been issued, the side
+    # stream waits for mark[s], reduces partials[s] (deterministic order) into reds[s] and
+    # all-reduces the two doubles over RCCL, overlapped with that launch; the stats launch that
+    # next reuses slot s first waits for the reducer's event of that slot.  Every event the
+    # region records is created and recorded once before it (torch creates a HIP event lazily at
+    # its first record, and Stream.wait_stream creates a fresh one per call), and every library
+    # call in it goes straight through the C ABI with pre-built arguments.
     partials = [torch.zeros((env.partial_count(), 2), dtype=torch.float32, device=dev)
                 for _ in range(2)]
     reds = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
-    released = [None, None]
     main_s = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev)
-    stats = pdist.StatsReducer(2, dev)
+    stats = pdist.StatsReducer(2, dev, stream=side)
+    mark = [torch.cuda.Event() for _ in range(2)]
+    freed = [None, None]  # the reducer event after which partials[s] may be rewritten
     env.reset_tensor()
     phase = args.episode_phase if args.reset_mode == "philox" else "aligned"
     if phase == "staggered":
         stagger_episodes(env, first)
     nstat = [0]
+    pending = []  # (launch index, slot) of stats launches whose reduction is not issued yet
 
-    # Full-length launches go straight through the C ABI (include/fenv.h fenv_rollout) with
-    # pre-built arguments: the Python face's per-call validation (~10-20 us of host time) would
-    # sit in front of the timed region's first launch.  The buffers are validated once, here,
-    # by a call through the Python face.
+    # Full-length launches go straight through the C ABI (include/fenv.h fenv_rollout,
+    # fenv_reduce_partials) with pre-built arguments: the Python face's per-call validation
+    # (~10-20 us of host time) would sit in front of the timed region's first launch.  The
+    # buffers are validated once, here, by calls through the Python face.
     import ctypes
     flib = import_module(pkg.__name__ + "._lib")
     L_abi = flib.lib()
@@ -584,53 +591,68 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     abi_args = [(env._h, T, vp(acts[k].data_ptr()), vp(obs.data_ptr()), vp(rew.data_ptr()),
                  vp(done.data_ptr())) for k in range(2)]
     abi_part = [vp(p.data_ptr()) for p in partials]
+    npart = env.partial_count()
+    abi_red = {(k, st): (abi_part[k], npart, vp(reds[k].data_ptr()), vp(st.cuda_stream))
+               for k in range(2) for st in (main_s, side)}
     env.rollout(acts[0], obs, rew, done, partial=partials[0])
+    env.reduce_partials(partials[0], reds[0])
+    for e in mark:
+        e.record(main_s)
 
-    def rollout_abi(k, stat):
-        rc = L_abi.fenv_rollout(*abi_args[k], abi_part[k] if stat else None, abi_stream)
+    def issue_stats(s, st):
+        """Reduce partials[s] into reds[s] and all-reduce it, on stream `st` (after mark[s])."""
+        if st is not main_s:
+            st.wait_event(mark[s])
+        rc = L_abi.fenv_reduce_partials(*abi_red[(s, st)])
         if rc:
-            flib.check(rc, "fenv_rollout")
+            flib.check(rc, "fenv_reduce_partials")
+        stats.submit(reds[s], stream=st)
+        freed[s] = stats.ready()
 
-    def launch(L, stat=False, last=False, ev=None):
-        """One fused rollout of L steps (actions of slot nstat-parity; stats if `stat`).  The
-        stats of the region's last launch are reduced on the main stream (nothing left to
-        overlap; saves two cross-queue hops before the closing synchronize).  `ev` is recorded
-        on the launch stream right before the kernel (after any stream-ordering call)."""
+    def flush(before=None, last=False):
+        """Issue the reductions of the pending stats launches (those before launch index
+        `before`; all if None).  A reduction with no launch left to hide under (`last`) runs on
+        the main stream: no cross-stream hop before the closing synchronize."""
+        while pending and (before is None or pending[0][0] < before):
+            _, s = pending.pop(0)
+            issue_stats(s, main_s if last else side)
+
+    def launch(k, L, stat=False, ev=None):
+        """Launch k of a region: one fused rollout of L steps (actions of slot nstat-parity;
+        stats if `stat`).  `ev` is recorded on the launch stream right before the kernel (after
+        any stream-ordering call)."""
         s = nstat[0] % 2
-        if stat and released[s] is not None:
-            main_s.wait_event(released[s])
+        if stat and freed[s] is not None:
+            main_s.wait_event(freed[s])
         if ev is not None:
             ev.record(main_s)
         if L == T:
-            rollout_abi(s, stat)
+            rc = L_abi.fenv_rollout(*abi_args[s], abi_part[s] if stat else None, abi_stream)
+            if rc:
+                flib.check(rc, "fenv_rollout")
         else:
             env.rollout(acts[s][:L], obs[:L], rew[:L], done[:L],
                         partial=partials[s] if stat else None)
         if stat:
-            red_s = main_s if last else side
-            if not last:
-                side.wait_stream(main_s)
-            with torch.cuda.stream(red_s):
-                stats.reserve()
-                env.reduce_partials(partials[s], reds[s])
-                stats.submit(reds[s])
-                released[s] = torch.cuda.Event()
-                released[s].record(red_s)
+            mark[s].record(main_s)
+            pending.append((k, s))
             nstat[0] += 1
 
     def region(plan, stat_every, evs=None):
         """The timed region's work: the launches of `plan`, stats on the first launch of every
-        `stat_every` (so a region of several launches never ends on a stats reduction: it runs
-        on the side stream under the next launch), then the wait for the stats (side stream /
+        `stat_every` (a stats launch's reduction is issued after the next launch, so it runs
+        on the side stream under that launch), then the wait for the last stats (side stream /
         all-reduce)."""
+        n = len(plan)
         for k, L in enumerate(plan):
-            launch(L, stat=not args.no_stats and k % stat_every == 0,
-                   last=k == len(plan) - 1, ev=evs[0] if (evs is not None and k == 0) else None)
+            launch(k, L, stat=not args.no_stats and k % stat_every == 0,
+                   ev=evs[0] if (evs is not None and k == 0) else None)
             if evs is not None:
                 evs[k + 1].record(main_s)
+            flush(before=k)
+        flush(last=bool(pending) and pending[-1][0] == n - 1)
         if not args.no_stats:
-            main_s.wait_stream(side)  # (a no-op dependency when the last launch reduced inline)
-            return stats.result()
+            return stats.result(main_s)
         return None
 
     # 1) pre-warm by device time: clocks, first touch of the 2 GB rollout buffer, and the first
@@ -660,13 +682,16 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     for _ in range(more):
         pw_ms += prewarm_region()
         pw_launches += 5
-    # the timed region's plan and events are made before the closing synchronize, so nothing but
-    # the barrier separates the warm-up launches from the first timed launch
+    # the timed region's plan and events are made (and each event recorded once) before the
+    # closing synchronize, so nothing but the barrier separates the warm-up launches from the
+    # first timed launch
     plan = launch_plan(args.steps, T)
     stat_every = max(1, min(args.stats_every, len(plan)))
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
+    for e in evs:
+        e.record(main_s)
     for L in launch_plan(args.warmup, T):
-        launch(L)
+        launch(-1, L)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -676,10 +701,11 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     tot = region(plan, stat_every, evs)
     t_issued = time.perf_counter() - t0
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
+    # the slowest rank, and a barrier inside would add a collective's latency to every rank
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
     per_launch = [evs[k].elapsed_time(evs[k + 1]) for k in range(len(plan))]
     ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
     # the same byte mix over the first 4 planes only: a 1 GB reuse footprint instead of 2.46 GB
@@ -695,6 +721,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     steps = sum(plan)
     total_agents = total_formations * N
     value = total_agents * steps / elapsed
+    # the same agent-steps over the slowest rank's event-timed kernel time: what the kernels
+    # scale to with the region's fixed host / synchronisation cost taken out (never `value`)
+    kernel_value = total_agents * steps / (kern_total_ms * 1e-3)
     bytes_launch = rollout_bytes_per_launch(A, N, D, T)
     bytes_timed = sum(rollout_bytes_per_launch(A, N, D, L) for L in plan)
     achieved = bytes_timed / (kern_total_ms * 1e-3) / 1e9
@@ -720,6 +749,8 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "warmup_launches": pw_launches,
             "warmup_ms": pw_ms,
             "host_issue_ms": t_issued * 1e3,
+            "kernel_value": kernel_value,
+            "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
             "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
@@ -839,7 +870,8 @@ def main():
         env2.release()
         del env2
         if rank == 0:
-            keep = ("value", "ms_per_step", "scaling", "config", "roofline", "steps")
+            keep = ("value", "kernel_value", "fixed_overhead_ms", "ms_per_step", "scaling",
+                    "config", "roofline", "steps")
             out[f"{other}_scaling_line"] = {k: o2[k] for k in keep}
     if rank == 0:
         if world == 1 and not args.no_policy:

@@ -12,6 +12,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <new>
 #include <thread>
 #include <unordered_set>
 #include <vector>
@@ -142,17 +143,26 @@ FENV_HOST_CLONES void formations_from_draws(const uint32_t *u, int64_t f0, int64
     }
 }
 
-// `count` formations' reset draws from the stream's current position, in chunks of ~48K draws
-// (an L2-resident buffer): a chunk's draws in one fill, then its formations in one pass.
-void draw_formations(Mt19937 &mt, int64_t N, int64_t count, float *px, float *py, float *gx,
-                     float *gy, uint32_t gen = 0, uint32_t *at = nullptr, uint32_t *gt = nullptr) {
+// Words of the chunk buffer draw_formations needs for `count` formations of N agents.
+size_t draw_scratch_words(int64_t N, int64_t count) {
     const int64_t per = 2 * N + 2;
     const int64_t chunk = std::max<int64_t>(1, 49152 / per);
-    std::vector<uint32_t> u((size_t)(std::min<int64_t>(chunk, std::max<int64_t>(count, 1)) * per));
+    return (size_t)(std::min<int64_t>(chunk, std::max<int64_t>(count, 1)) * per);
+}
+
+// `count` formations' reset draws from the stream's current position, in chunks of ~48K draws
+// (an L2-resident buffer, `u`, at least draw_scratch_words(N, count) words): a chunk's draws in
+// one fill, then its formations in one pass.  Allocates nothing, so it cannot throw: the
+// draw-ahead thread runs it.
+void draw_formations(Mt19937 &mt, int64_t N, int64_t count, uint32_t *u, float *px, float *py,
+                     float *gx, float *gy, uint32_t gen = 0, uint32_t *at = nullptr,
+                     uint32_t *gt = nullptr) {
+    const int64_t per = 2 * N + 2;
+    const int64_t chunk = std::max<int64_t>(1, 49152 / per);
     for (int64_t f0 = 0; f0 < count; f0 += chunk) {
         const int64_t cnt = std::min<int64_t>(chunk, count - f0);
-        mt.fill(u.data(), (size_t)(cnt * per));
-        formations_from_draws(u.data(), f0, cnt, N, px, py, gx, gy, gen, at, gt);
+        mt.fill(u, (size_t)(cnt * per));
+        formations_from_draws(u, f0, cnt, N, px, py, gx, gy, gen, at, gt);
     }
 }
 
@@ -331,6 +341,9 @@ struct fenv {
     // cannot disturb a stream capture elsewhere in the process.  mt and that host slot belong
     // to the thread until it is joined (join_ahead), and nothing else touches mt.
     std::thread ahead;
+    // draw_set's chunk buffer, sized at fenv_create: the thread's body allocates nothing, so no
+    // std::bad_alloc can escape it (an exception leaving a std::thread calls std::terminate)
+    std::vector<uint32_t> draw_buf;
     int ahead_slot = -1;     // host slot the thread is drawing into (-1: none)
     uint32_t ahead_gen = 0;  // the generation it is drawing
 
@@ -371,7 +384,8 @@ struct fenv {
         mt.discard(per * (uint64_t)c.f0);
         float *hp = hpend + off;
         uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F);
-        draw_formations(mt, c.N, c.F, hp, hp + A, hp + 2 * A, hp + 2 * A + c.F, gen, at, at + A);
+        draw_formations(mt, c.N, c.F, draw_buf.data(), hp, hp + A, hp + 2 * A, hp + 2 * A + c.F,
+                        gen, at, at + A);
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
     }
 
@@ -419,6 +433,7 @@ struct fenv {
         const int nx = w ^ 1;
         if (pend_ev_recorded[nx]) FENV_HIP(hipEventSynchronize(pend_ev[nx]));
         try {
+            // draw_set allocates nothing (draw_buf is sized at fenv_create): the body cannot throw
             ahead = std::thread([this, nx, g = gen_next]() { draw_set(nx, g); });
             ahead_slot = nx;
             ahead_gen = gen_next++;
@@ -482,7 +497,8 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
     drain_graveyard();
     FENV_HIP(hipSetDevice(device));
 
-    fenv *e = new fenv();
+    fenv *e = new (std::nothrow) fenv();
+    if (!e) return fail(FENV_ENOMEM, "fenv_create: out of host memory");
     live_add(e);
     e->device = device;
     e->goal_in_obs = goal_in_obs ? 1 : 0;
@@ -548,6 +564,11 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
             he = hipEventCreateWithFlags(&e->pend_ev[k], hipEventDisableTiming);
             if (he == hipSuccess) he = hipEventCreateWithFlags(&e->used_ev[k], hipEventDisableTiming);
             if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipEventCreate failed"));
+        }
+        try {
+            e->draw_buf.resize(draw_scratch_words(num_agents, num_formation));
+        } catch (const std::bad_alloc &) {
+            return cleanup(fail(FENV_ENOMEM, "draw buffer allocation failed"));
         }
     }
     // FormationEnv ctor: every FormationSimulator.__init__ calls reset() (simulate.py:61).
@@ -852,11 +873,17 @@ int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64
     if (num_agents < 1 || total < 0 || first < 0 || count < 0 || first + count > total ||
         skip_sets < 0 || (count > 0 && (!px || !py || !gx || !gy)))
         return fail(FENV_EINVAL, "fenv_host_reset_draws: bad arguments");
+    std::vector<uint32_t> u;
+    try {
+        u.resize(draw_scratch_words(num_agents, count));
+    } catch (const std::bad_alloc &) {
+        return fail(FENV_ENOMEM, "fenv_host_reset_draws: out of host memory");
+    }
     Mt19937 mt;
     mt.seed(seed);
     const uint64_t per = 2ull * (uint64_t)num_agents + 2ull;
     mt.discard(per * ((uint64_t)skip_sets * (uint64_t)total + (uint64_t)first));
-    draw_formations(mt, num_agents, count, px, py, gx, gy);
+    draw_formations(mt, num_agents, count, u.data(), px, py, gx, gy);
     return FENV_OK;
 }
 

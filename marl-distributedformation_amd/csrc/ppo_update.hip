@@ -1002,7 +1002,9 @@ __global__ __launch_bounds__(SPLIT ? kPTS : kPT) void k_ppo_update(PPOArgs g) {
                 const float *zmw = R + kZM + 4 * net;  // this network's four wave maxima
                 const float zm = fmaxf(fmaxf(zmw[0], zmw[1]), fmaxf(zmw[2], zmw[3]));
                 int se = 264 - (int)((__float_as_uint(zm) >> 23) & 0xFFu);  // 127 + 10 - e
-                se = se < 1 ? 1 : (se > 254 ? 254 : se);
+                // <= 253 keeps the unscale factor 2^(127 - se) a normal number (254 made it +0
+                // and zeroed the W2 / dL/dh1 gradients of a network whose max |dL/dz2| < 2^-116)
+                se = se < 1 ? 1 : (se > 253 ? 253 : se);
                 const float zs = __uint_as_float((uint32_t)se << 23);
                 const float zi = __uint_as_float((uint32_t)(254 - se) << 23);
                 const float *pa = Z2 + (32 * h) * kRow + 32 * mt + c;

@@ -46,20 +46,33 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
 class StatsReducer:
     """Stream-overlapped all-reduce of a small stats vector, two submissions in flight.
 
-    ``submit(v)`` starts an async all-reduce of ``v`` IN PLACE on a side stream (after the
-    current stream's work that produced v); the caller alternates two buffers and must not
-    overwrite a buffer until the submission two calls later (``submit`` then waits for the
-    collective that used the same slot).  ``result()`` waits and returns the last buffer.
-    With world_size 1 there is nothing to reduce and ``v`` is returned as is."""
+    ``submit(v)`` starts an async all-reduce of ``v`` IN PLACE on a side stream, after the
+    current stream's work that produced v (or after the event ``after``); the caller alternates
+    two buffers and must not overwrite a buffer until the submission two calls later (``submit``
+    then waits for the collective that used the same slot).  ``result()`` makes the current
+    stream (or ``stream``) wait for the last submission and returns its buffer.  With world
+    size 1 there is nothing to reduce and ``v`` is returned as is.
 
-    def __init__(self, n: int, device):
+    Every cross-stream dependency goes through events created and recorded once in the
+    constructor: torch's ``Stream.wait_stream`` creates and records a fresh event per call, and
+    a torch event is created lazily at its first record -- host work that would otherwise sit
+    inside a caller's timed region (bench.py).  ``stream`` lets the caller hand in the side
+    stream it already reduces on, so the collective adds no stream hop."""
+
+    def __init__(self, n: int, device, stream=None):
         self.device = torch.device(device)
         self.work = [None, None]
         self.bufs = [None, None]
         self.k = 0
         self.cuda = self.device.type == "cuda"
-        self.side = torch.cuda.Stream(self.device) if self.cuda else None
         self.dist = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.side = None
+        if self.cuda:
+            self.side = stream if stream is not None else torch.cuda.Stream(self.device)
+            self.dep = torch.cuda.Event()
+            self.done = [torch.cuda.Event(), torch.cuda.Event()]
+            for e in [self.dep] + self.done:
+                e.record(self.side)
 
     def reserve(self) -> None:
         """Make the current stream wait until the next slot's previous all-reduce finished
@@ -69,26 +82,41 @@ class StatsReducer:
             self.work[s].wait()
             self.work[s] = None
 
-    def submit(self, v: torch.Tensor) -> None:
-        self.reserve()
+    def submit(self, v: torch.Tensor, after=None, stream=None) -> None:
+        """All-reduce ``v`` in place: on ``stream`` if given (v was produced on it, or the caller
+        ordered it there), after ``after`` if given, else on the side stream after the current
+        stream's work so far."""
         s = self.k % 2
         self.bufs[s] = v
-        if self.dist:
-            if self.cuda:
-                self.side.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(self.side):
-                    self.work[s] = dist.all_reduce(v, async_op=True)
-            else:
+        if self.cuda:
+            st = stream if stream is not None else self.side
+            if after is not None:
+                st.wait_event(after)
+            elif stream is None:
+                self.dep.record(torch.cuda.current_stream(self.device))
+                st.wait_event(self.dep)
+            with torch.cuda.stream(st):
+                if self.dist:
+                    # stream-ordered: wait() only makes the side stream wait for the collective
+                    dist.all_reduce(v, async_op=True).wait()
+                self.done[s].record(st)
+        else:
+            self.reserve()
+            if self.dist:
                 self.work[s] = dist.all_reduce(v, async_op=True)
         self.k += 1
 
-    def result(self) -> torch.Tensor:
+    def ready(self):
+        """The event of the last submission (cuda), None before the first or on the CPU."""
+        return self.done[(self.k - 1) % 2] if self.cuda and self.k else None
+
+    def result(self, stream=None) -> torch.Tensor:
         s = (self.k - 1) % 2
         if self.work[s] is not None:
             self.work[s].wait()
             self.work[s] = None
         if self.cuda:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            (stream or torch.cuda.current_stream(self.device)).wait_event(self.done[s])
         return self.bufs[s]
 
 

@@ -138,6 +138,38 @@ def torch_rand_from_raw(raw: np.ndarray) -> np.ndarray:
     return (raw & np.uint32(0xFFFFFF)).astype(np.float32) * np.float32(2.0 ** -24)
 
 
+def mt_reset_draws(seed: int, sets, total: int, formations: np.ndarray, num_agents: int):
+    """The reference's reset draws for selected formations, straight from the global MT19937
+    stream (numpy's MT19937 with init_genrand seeding == torch.manual_seed, vectorized_env.py:
+    52-55): draw set s of a ``total``-formation env is the stream's words
+    [s * total * (2N + 2), (s + 1) * total * (2N + 2)), formation f's part of it the 2N + 2 words
+    from f * (2N + 2) on -- N (x, y) pairs, then the goal pair (simulate.py:133-143, torch.rand =
+    (u32 & 0xFFFFFF) * 2^-24; x * 400, y * 100, goal (x * 280 + 60, y * 480 + 60)).  Set 0 is the
+    constructor's reset, 1 the first reset(), then one set per timeout.  Independent of the
+    library's block-twisted generator and its draw-ahead thread (fenv_api.cpp), which it checks.
+    Returns {s: (px [k * N], py [k * N], gx [k], gy [k])} for every s in ``sets``."""
+    N = int(num_agents)
+    per = 2 * N + 2
+    f = np.asarray(formations, np.int64)
+    bg = np.random.MT19937()
+    bg._legacy_seeding(int(seed) & 0xFFFFFFFF)
+    out = {}
+    want = sorted(set(int(s) for s in sets))
+    cols = (f[:, None] * per + np.arange(per)).reshape(-1)
+    for s in range(want[-1] + 1):
+        raw = bg.random_raw(total * per)  # one whole set (the stream continues across calls)
+        if s not in want:
+            continue
+        u = torch_rand_from_raw(raw[cols].astype(np.uint32)).reshape(len(f), per)
+        px = (u[:, 0:2 * N:2] * np.float32(400.0)).astype(np.float32).reshape(-1)
+        py = (u[:, 1:2 * N:2] * np.float32(100.0)).astype(np.float32).reshape(-1)
+        gx = (u[:, 2 * N] * np.float32(280.0) + np.float32(60.0)).astype(np.float32)
+        gy = (u[:, 2 * N + 1] * np.float32(480.0) + np.float32(60.0)).astype(np.float32)
+        out[s] = (px, py, gx, gy)
+        del raw
+    return out
+
+
 # ----------------------------------------------------------------------------- exact fmaf
 def fmaf(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
     """Correctly rounded fp32 fma(a, b, c) for fp32 arrays (one rounding, like v_fma_f32)."""

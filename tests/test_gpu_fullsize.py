@@ -314,3 +314,72 @@ def test_bench_workload_staggered_resets_vs_oracle(venv):
     rsum = rew.double().sum().item()
     assert abs(sums[0] - rsum) <= 1e-5 * max(1.0, abs(rsum)), (sums[0], rsum)
     assert sums[1] == float(done.sum().item())
+
+
+def test_mt19937_config3_resets_vs_stream(venv):
+    """MT19937 reset mode (the reference's exact RNG) at BASELINE config 3
+    (1,048,576 x 5), where each draw set is 12.6M MT19937 words drawn by the library's
+    block-twisted generator on its draw-ahead thread, staged through the pinned pool and copied
+    by k_stage_copy (fenv_api.cpp).  max_steps 7 (episodes of 9 steps) puts two reset events
+    inside the two fused 10-step launches (steps 9 and 18; the library splits each launch
+    there).  Sampled formations -- random ones, the grid's ends and both sides of every
+    4,096-formation draw chunk -- are checked against numpy's MT19937 at their stream offsets
+    (oracle.mt_reset_draws, not the library's own generator): the reset() state (set 1) and each
+    post-reset state (sets 2, 3); the C oracle replays every step between, bit for bit: the done
+    step's reward and done on the pre-reset state, the post-reset observation, the final state."""
+    from oracle import mt_reset_draws
+    F, N, T, ms, seed = 1 << 20, 5, 10, 7, 4242
+    ep = ms + 2
+    env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
+                             "goal_in_obs": True}, device=DEV, seed=seed, reset_mode="mt19937",
+                            max_steps=ms)
+    A = F * N
+    env.reset_tensor()
+    px0, py0, gx0, gy0, t0 = env.get_state()
+    g = torch.Generator(device=DEV).manual_seed(77)
+    acts = [torch.rand((T, A, 2), device=DEV, generator=g) * 2.4 - 1.2 for _ in range(2)]
+    out = [env.rollout(a) for a in acts]
+    px1, py1, gx1, gy1, t1 = env.get_state()
+    torch.cuda.synchronize()
+
+    rng = np.random.default_rng(9)
+    chunk = 49152 // (2 * N + 2)  # formations per draw chunk (fenv_api.cpp draw_formations)
+    edges = np.arange(chunk, F, chunk)
+    fs = np.unique(np.concatenate([rng.choice(F, 1500, replace=False), [0, 1, F - 2, F - 1],
+                                   edges - 1, edges])).astype(np.int64)
+    ag = (fs[:, None] * N + np.arange(N)).reshape(-1)
+    agt, fst = torch.from_numpy(ag).to(DEV), torch.from_numpy(fs).to(DEV)
+    want = mt_reset_draws(seed, [1, 2, 3], F, fs, N)
+    st = [px0[agt].cpu().numpy(), py0[agt].cpu().numpy(), gx0[fst].cpu().numpy(),
+          gy0[fst].cpu().numpy(), t0[fst].cpu().numpy()]
+    for name, a, b in zip(("px", "py", "gx", "gy"), st[:4], want[1]):
+        assert np.array_equal(bits(a), bits(b)), f"reset() state {name}"
+    assert np.all(st[4] == 0)
+    ref = COracleEnv(len(fs), N, True, 0, max_steps=ms)
+    ref.set_state(*st)
+    resets = 0
+    for k in range(2 * T):
+        la, j = divmod(k, T)
+        obs, rew, done = out[la]
+        a_s = acts[la][j, agt].cpu().numpy()
+        _, rr, rd, _ = ref.step(np.ascontiguousarray(a_s))
+        assert np.array_equal(bits(rew[j, agt].cpu().numpy()), bits(rr)), f"reward step {k + 1}"
+        assert np.array_equal(done[j, agt].cpu().numpy(), rd), f"done step {k + 1}"
+        if (k + 1) % ep == 0:  # every formation times out together (lock-step episodes)
+            assert rd.all() and bool(done[j].all()), f"step {k + 1}"
+            resets += 1
+            px, py, gx, gy, t = ref.get_state()
+            px, py, gx, gy = want[1 + resets]  # the oracle drew from its own sample-local stream
+            assert np.all(t == 0)
+            ref.set_state(px, py, gx, gy, t)
+        else:
+            assert not rd.any() and not bool(done[j].any()), f"step {k + 1}"
+        ro = ref.observe()
+        assert np.array_equal(bits(obs[j, agt].cpu().numpy()), bits(ro)), f"obs step {k + 1}"
+    assert resets == 2
+    rs = ref.get_state()
+    for name, v, w, idx in (("px", px1, rs[0], agt), ("py", py1, rs[1], agt),
+                            ("gx", gx1, rs[2], fst), ("gy", gy1, rs[3], fst),
+                            ("t", t1, rs[4], fst)):
+        assert np.array_equal(bits(v[idx].cpu().numpy()), bits(w)), name
+    env.release()

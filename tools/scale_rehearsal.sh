@@ -1,0 +1,35 @@
+#!/bin/bash
+# bench.py's timed region at the shard sizes of an 8/4/2/1-GPU strong-scaling run of config 3
+# (131072, 262144, 524288, 1048576 formations on one GPU, the driver's --steps 20 --warmup 5):
+# wall vs event-timed kernel time and the fixed overhead per size; then the bench's N > 1 path
+# with two ranks on the one GPU over gloo (its rate says nothing about scaling).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-r5}
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export PYTHONUNBUFFERED=1
+for F in ${SIZES:-131072 262144 524288 1048576}; do
+  for rep in 1 2 3; do
+    timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 --formations $F --no-policy \
+      --no-configs --no-cpu-baseline > "$O/shard_${F}_$rep.json" 2> "$O/shard_${F}_$rep.err" || exit $?
+  done
+done
+python - "$O" <<'PY'
+import glob, json, sys
+rows = {}
+for f in sorted(glob.glob(sys.argv[1] + "/shard_*_*.json")):
+    d = json.load(open(f))
+    F = d["config"]["formations"]
+    rows.setdefault(F, []).append((d["ms_per_step"] * d["steps"], d["roofline"]["kernel_ms_timed"],
+                                   d["fixed_overhead_ms"] * 1e3, d["value"], d["kernel_value"]))
+for F, v in sorted(rows.items()):
+    print(F, " | ".join(f"wall {a:.4f} ms kern {b:.4f} ms fixed {c:.1f} us value {e:.3e} kv {g:.3e}"
+                        for a, b, c, e, g in v))
+PY
+if [ -z "${SKIP_GLOO:-}" ]; then
+  FENV_DIST_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 \
+    --formations 262144 > "$O/rehearse_2rank.json" 2> "$O/rehearse_2rank.err"
+  rc=$?; echo "2-rank rc=$rc"; cut -c1-400 "$O/rehearse_2rank.json"; exit $rc
+fi
