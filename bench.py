@@ -453,7 +453,7 @@ def ppo_update_bench(pkgname: str, dev, formations: int = 1000, agents: int = 5,
 
 def ppo_pmc_mfma():
     """Counter-backed MFMA-pipe occupancy of k_ppo_update from the committed PMC passes
-    (tools/job_r4_ppopmc.sh -> profiles/r4_ppo_pmc_sq.json, else round 3's; not measured in this
+    (tools/ppo_pmc.sh -> profiles/r4_ppo_pmc_sq.json, else round 3's; not measured in this
     run).  The kernel runs 8 waves on 8 SIMDs (4 per CU, actor and critic CU);
     SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over the chip, GRBM_GUI_ACTIVE the kernel's
     cycles summed over the 8 XCDs."""
@@ -622,10 +622,13 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         stats if `stat`).  `ev` is recorded on the launch stream right before the kernel (after
         any stream-ordering call)."""
         s = nstat[0] % 2
-        if stat and freed[s] is not None:
+        if stat and freed[s] is not None and not freed[s].query():
+            # (a reduction the host already saw complete needs no wait packet in the queue)
             main_s.wait_event(freed[s])
+        stamp("stats wait")
         if ev is not None:
             ev.record(main_s)
+            stamp("start event")
         if L == T:
             rc = L_abi.fenv_rollout(*abi_args[s], abi_part[s] if stat else None, abi_stream)
             if rc:
@@ -638,22 +641,37 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             pending.append((k, s))
             nstat[0] += 1
 
+    trace = [] if args.trace_host else None
+
+    def stamp(what):
+        if trace is not None:
+            trace.append((what, time.perf_counter()))
+
     def region(plan, stat_every, evs=None):
         """The timed region's work: the launches of `plan`, stats on the first launch of every
         `stat_every` (a stats launch's reduction is issued after the next launch, so it runs
         on the side stream under that launch), then the wait for the last stats (side stream /
-        all-reduce)."""
+        all-reduce).  `evs` = (start, end) timing events: start right before the first kernel,
+        end right after the last.  No timing event goes between launches: the command processor
+        idles the GPU ~12 us at each one (it completes the kernel and writes back the caches
+        before it takes the timestamp; rocprofv3 kernel trace, profiles/r5_region_trace.txt),
+        where a launch after a plain kernel or a timing-free event starts at once."""
         n = len(plan)
         for k, L in enumerate(plan):
             launch(k, L, stat=not args.no_stats and k % stat_every == 0,
                    ev=evs[0] if (evs is not None and k == 0) else None)
-            if evs is not None:
-                evs[k + 1].record(main_s)
+            stamp(f"launch {k}")
+            if evs is not None and k == n - 1:
+                evs[1].record(main_s)
             flush(before=k)
+            stamp(f"stats before {k}")
         flush(last=bool(pending) and pending[-1][0] == n - 1)
-        if not args.no_stats:
-            return stats.result(main_s)
-        return None
+        stamp("last stats")
+        # The last stats' buffer; nothing on the device consumes it, so no stream waits for the
+        # side stream here: the caller's device-wide synchronize (every stream, RCCL's included)
+        # completes it before the host reads it.
+        stamp("region issued")
+        return None if args.no_stats else stats.bufs[(stats.k - 1) % 2]
 
     # 1) pre-warm by device time: clocks, first touch of the 2 GB rollout buffer, and the first
     # use of every kernel, stream and event the timed region uses (a kernel's first launch or a
@@ -687,7 +705,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     # first timed launch
     plan = launch_plan(args.steps, T)
     stat_every = max(1, min(args.stats_every, len(plan)))
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(plan) + 1)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for e in evs:
         e.record(main_s)
     for L in launch_plan(args.warmup, T):
@@ -696,29 +714,30 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    freed[0] = freed[1] = None  # the synchronize completed every reduction (no wait packets)
 
+    if trace is not None:
+        trace.clear()
     t0 = time.perf_counter()
     tot = region(plan, stat_every, evs)
     t_issued = time.perf_counter() - t0
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    stamp("synchronized")
     # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
     # the slowest rank, and a barrier inside would add a collective's latency to every rank
     if world > 1:
         torch.distributed.barrier()
-    per_launch = [evs[k].elapsed_time(evs[k + 1]) for k in range(len(plan))]
+    kern_total_ms = evs[0].elapsed_time(evs[1])
     ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
     # the same byte mix over the first 4 planes only: a 1 GB reuse footprint instead of 2.46 GB
     # (the launch's own footprint is what separates the two)
     ceiling_small = hbm_ceiling(acts[0], obs, rew, done, A, min(T, 4), D, main_s)
-    kern_total_ms = sum(per_launch)
-    full = [ms for ms, L in zip(per_launch, plan) if L == T] or per_launch
-    kern_avg_ms = sum(full) / len(full)
     elapsed = pdist.max_over_ranks(elapsed, dev)
     kern_total_ms = pdist.max_over_ranks(kern_total_ms, dev)
-    kern_avg_ms = pdist.max_over_ranks(kern_avg_ms, dev)
 
     steps = sum(plan)
+    kern_avg_ms = kern_total_ms * T / steps  # per T-step launch (equal to the mean when uniform)
     total_agents = total_formations * N
     value = total_agents * steps / elapsed
     # the same agent-steps over the slowest rank's event-timed kernel time: what the kernels
@@ -751,6 +770,8 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "host_issue_ms": t_issued * 1e3,
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
+            **({"host_trace_us": [(w, round((t - t0) * 1e6, 2)) for w, t in trace]}
+               if trace is not None else {}),
             "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
@@ -770,9 +791,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                          "algorithmic_bytes_timed": bytes_timed,
                          "avg_kernel_ms": kern_avg_ms, "kernel_ms_timed": kern_total_ms,
                          "launches": len(plan),
-                         "launch_ms_min": min(per_launch), "launch_ms_max": max(per_launch),
-                         "launch_ms_first": per_launch[:8],
-                         "timing": "HIP events on the launch stream at every launch boundary"},
+                         "timing": "two HIP events on the launch stream, before the first and "
+                                   "after the last timed launch (none between launches: each "
+                                   "would idle the GPU ~12 us)"},
         }
         if ceiling is not None:
             ceiling["frac_of_spec"] = ceiling["achieved"] / HBM_PEAK_GBS
@@ -827,6 +848,8 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--trace-host", action="store_true",
+                    help="diagnostic: host timestamps (us after t0) of the timed region's calls")
     ap.add_argument("--stats-every", type=int, default=10,
                     help="reduce + all-reduce the episode stats every this many rollout launches "
                          "(clamped to the timed launch count)")

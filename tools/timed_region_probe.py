@@ -13,6 +13,8 @@ median wall time, the median event-timed kernel time and their difference (the f
                  records a fresh event) around a side-stream stats reduction of launch 1
   waitevent      the same dependencies through pre-created events (wait_event)
   waitevent_late waitevent with launch 2 issued before launch 1's side-stream stats work
+  bench_*        bench.py's region (timing events at the ends only), ended by a device
+                 synchronize, by polling the last event first, or by synchronizing on it first
 
     python tools/timed_region_probe.py [F ...]        (default 131072 1048576)
 """
@@ -34,7 +36,7 @@ from importlib import import_module  # noqa: E402
 venv = import_module(pkg.__name__ + ".vectorized_env")
 flib = import_module(pkg.__name__ + "._lib")
 dev = torch.device("cuda", 0)
-T, N, R = 10, 5, 40
+T, N, R = 10, 5, int(os.environ.get("PROBE_REPS", 40))
 vp = ctypes.c_void_p
 
 
@@ -154,9 +156,38 @@ def probe(F):
         fin.synchronize()
         return time.perf_counter() - t0, pre[0].elapsed_time(pre[2])
 
+    def bench_like(end):
+        """bench.py's region at HEAD: start event, stats launch, plain mark, launch, end event,
+        side-stream reduction issued after the second launch, main waits for it, fin; then the
+        end of the window by `end`: devsync, poll (fin.query() loop, then devsync), evsync
+        (fin.synchronize(), then devsync)."""
+        def f():
+            t0 = time.perf_counter()
+            pre[0].record(main)
+            launch(True)
+            dep[0].record(main)
+            launch()
+            pre[2].record(main)
+            side.wait_event(dep[0])
+            reduce_side()
+            dep[1].record(side)
+            main.wait_event(dep[1])
+            fin.record(main)
+            if end == "poll":
+                while not fin.query():
+                    pass
+            elif end == "evsync":
+                fin.synchronize()
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0, pre[0].elapsed_time(pre[2])
+        return f
+
     variants = dict(bare_devsync=bare_devsync, bare_evsync=bare_evsync, ev_fresh=ev_fresh,
                     ev_pre=ev_pre, waitstream=waitstream, waitevent=waitevent,
-                    waitevent_late=waitevent_late)
+                    waitevent_late=waitevent_late, bench_devsync=bench_like("devsync"),
+                    bench_poll=bench_like("poll"), bench_evsync=bench_like("evsync"))
+    if os.environ.get("PROBE_ONLY"):
+        variants = {k: v for k, v in variants.items() if k in os.environ["PROBE_ONLY"].split(",")}
     # device time of two launches, for the variants without events
     kern = []
     for _ in range(R):
