@@ -87,18 +87,41 @@ REFERENCE_CPU_MEASURED = {
     "source": "SURVEY.md §6 / BASELINE.md (measured by importing /root/reference; not re-run)"}
 
 
+def cpu_share() -> tuple[int, str]:
+    """Host threads this job may run at once: the affinity mask, capped by the cgroup CPU quota
+    (cpu.max `quota period`).  On the GPU box the affinity shows all 256 CPUs and the quota is
+    1600000 / 100000 = 16 CPUs; the C port's rate there peaks at 16 threads (4.5e8) and falls
+    beyond (24: 4.4e8, 32: 4.2e8, 64: 2.0e8 -- throttled; tools/cpu_share_probe.py,
+    profiles/r5_cpu_share.json).  Returns (threads, how they were found)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for p in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(p).read().split()
+        except OSError:
+            continue
+        if p.endswith("cpu.max") and len(parts) == 2 and parts[0] != "max":
+            quota = int(parts[0]) / int(parts[1])
+        elif p.endswith("cfs_quota_us") and parts and int(parts[0]) > 0:
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = int(parts[0]) / period
+        break
+    if quota is None:
+        return max(1, aff), f"affinity {aff}, no cgroup CPU quota"
+    return max(1, min(aff, int(quota))), f"affinity {aff}, cgroup CPU quota {quota:g}"
+
+
 def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
     """Time the bit-exact C port of the reference env (oracle/fenv_oracle.c) on bounded samples:
     BASELINE config 0 (1000 x 5, the reference's default CPU run) and config 1 (4096 x 5) on one
     thread, then a sample of the headline workload (65,536 x 5 formations, one thread, then one
-    thread per host core of this job's CPU share, <= 16 on the GPU box, over formation shards).
+    thread per CPU of this job's share (cpu_share: 16 on the GPU box), over formation shards).
     `value` is the multi-threaded rate on the headline sample; `cores` the threads it used."""
     F = 65536
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    threads = max(1, min(16, share))
+    threads, share = cpu_share()
     small = budget_s / 6
     configs = {}
     for name, (fc, nc) in (("config0", (1000, 5)), ("config1", (4096, 5))):
@@ -114,8 +137,8 @@ def cpu_baseline(N: int, D: int, budget_s: float) -> dict:
                       f"({one_el:.1f} s), then {threads} threads over {threads} formation "
                       f"shards >= {many_steps} env steps each ({many_el:.1f} s); "
                       f"oracle/fenv_oracle.c (bit-exact C port of simulate.py/"
-                      f"vectorized_env.py); host reports {os.cpu_count()} CPUs, "
-                      f"affinity {share}",
+                      f"vectorized_env.py); host reports {os.cpu_count()} CPUs; "
+                      f"threads = this job's CPU share ({share})",
             "configs": configs,
             "reference_measured": REFERENCE_CPU_MEASURED}
 

@@ -25,3 +25,9 @@ def test_rollout_bytes_model():
     plan = bench.launch_plan(25, 10)
     tot = sum(bench.rollout_bytes_per_launch(A, N, D, L) for L in plan)
     assert tot > 25 * A * 45
+
+
+def test_cpu_share_within_affinity():
+    import os
+    threads, how = bench.cpu_share()
+    assert 1 <= threads <= len(os.sched_getaffinity(0)) and "affinity" in how
