@@ -24,6 +24,7 @@ update, MT19937 reset mode, the random-action launch, the numpy (PCIe-inclusive)
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -741,11 +742,16 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
 
     if trace is not None:
         trace.clear()
+    # no cyclic-GC pass inside the window (as timeit does): a generation-2 collection over the
+    # torch objects alive here takes far longer than the 20-step window
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     tot = region(plan, stat_every, evs)
     t_issued = time.perf_counter() - t0
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     stamp("synchronized")
     # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
     # the slowest rank, and a barrier inside would add a collective's latency to every rank
