@@ -384,7 +384,7 @@ def numpy_face_bench(pkgname: str, dev, formations: int, agents: int, steps: int
 def mt_mode_bench(pkgname: str, dev, formations: int, agents: int, steps: int = 2100,
                   T: int = 10) -> dict:
     """The same fused rollouts in MT19937 reset mode (the reference's exact RNG stream: every
-    reset set replayed on the host and staged, DESIGN.md §9.2), over a window holding two reset
+    reset set replayed on the host and staged, DESIGN.md §9.3), over a window holding two reset
     events (episode = 1,002 steps), with the Philox rate of the same window beside it."""
     import torch
     from importlib import import_module

@@ -261,7 +261,7 @@ def test_fused_update_vs_torch_at_reference_config(mods):
     * for the parameters, a coherent part K * lr * delta = 7,820 * 1e-3 * 4e-6 (delta = twice the
       per-minibatch gradient agreement test_ppo_grad_matches_autograd measures);
     * for every loss mean, 1e-5 relative (the north star's fp32 bound).
-    Round 4 (DESIGN.md §8): the kernel's Adam used 1 - fp32(beta) for the moment rates where torch
+    Round 4 (DESIGN.md §4.8): the kernel's Adam used 1 - fp32(beta) for the moment rates where torch
     uses fp32(1 - beta) formed in double (1.3e-5 relative apart for beta2 = 0.999, a coherent bias
     of every second moment) and exp2f(step * log2f(beta)) for beta^step (up to 1 ulp off); with
     torch's forms the update lands 2-200x closer to torch (profiles/ab/r4_ppo_precision_ab.txt), and

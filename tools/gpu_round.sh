@@ -31,7 +31,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 python3 "$R/tools/pmc_summary.py" "$R/gpurun_out" "$TAG" > "$O/pmc_summary.txt" 2>&1; echo "pmc summary rc=$?"
 # Last: rocprofv3 (ROCm 7.2) segfaults inside exit(), after its output is written, when the
-# profiled process made a cooperative launch (the PPO update's split launch; DESIGN §8 round 4,
+# profiled process made a cooperative launch (the PPO update's split launch; DESIGN §9.4,
 # profiles/r4_rocprof_coop_exit/), so nothing may follow it in this call.
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_driver" -o bench \
   -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver_under_rocprof.json" 2> "$O/prof_driver.err" \

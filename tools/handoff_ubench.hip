@@ -66,7 +66,7 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const int iters = 20000;
-    // work 0: the bare exchange; 18k cycles ~ one minibatch's per-block work (DESIGN §8)
+    // work 0: the bare exchange; 18k cycles ~ one minibatch's per-block work (DESIGN §4.8)
     const int works[] = {0, 18000};
     const int skews[] = {0, 700};
     for (int w : works)
