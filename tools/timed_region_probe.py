@@ -13,6 +13,8 @@ median wall time, the median event-timed kernel time and their difference (the f
                  records a fresh event) around a side-stream stats reduction of launch 1
   waitevent      the same dependencies through pre-created events (wait_event)
   waitevent_late waitevent with launch 2 issued before launch 1's side-stream stats work
+  ev_start_only / ev_end_only / ev_both: bare_devsync with a timing event before the first
+                 launch, after the last, or both (what each end's event costs)
   bench_*        bench.py's region (timing events at the ends only), ended by a device
                  synchronize, by polling the last event first, or by synchronizing on it first
 
@@ -182,7 +184,33 @@ def probe(F):
             return time.perf_counter() - t0, pre[0].elapsed_time(pre[2])
         return f
 
-    variants = dict(bare_devsync=bare_devsync, bare_evsync=bare_evsync, ev_fresh=ev_fresh,
+    def ev_start_only():
+        t0 = time.perf_counter()
+        pre[0].record(main)
+        launch()
+        launch()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, None
+
+    def ev_end_only():
+        t0 = time.perf_counter()
+        launch()
+        launch()
+        pre[2].record(main)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, None
+
+    def ev_both():
+        t0 = time.perf_counter()
+        pre[0].record(main)
+        launch()
+        launch()
+        pre[2].record(main)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, pre[0].elapsed_time(pre[2])
+
+    variants = dict(ev_start_only=ev_start_only, ev_end_only=ev_end_only, ev_both=ev_both,
+                    bare_devsync=bare_devsync, bare_evsync=bare_evsync, ev_fresh=ev_fresh,
                     ev_pre=ev_pre, waitstream=waitstream, waitevent=waitevent,
                     waitevent_late=waitevent_late, bench_devsync=bench_like("devsync"),
                     bench_poll=bench_like("poll"), bench_evsync=bench_like("evsync"))
