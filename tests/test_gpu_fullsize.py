@@ -316,7 +316,8 @@ def test_bench_workload_staggered_resets_vs_oracle(venv):
     assert sums[1] == float(done.sum().item())
 
 
-def test_mt19937_config3_resets_vs_stream(venv):
+@pytest.mark.parametrize("F,N", [(1 << 20, 5), (65536, 10), (16384, 64)])
+def test_mt19937_config3_resets_vs_stream(venv, F, N):
     """MT19937 reset mode (the reference's exact RNG) at BASELINE config 3
     (1,048,576 x 5), where each draw set is 12.6M MT19937 words drawn by the library's
     block-twisted generator on its draw-ahead thread, staged through the pinned pool and copied
@@ -326,9 +327,11 @@ def test_mt19937_config3_resets_vs_stream(venv):
     4,096-formation draw chunk -- are checked against numpy's MT19937 at their stream offsets
     (oracle.mt_reset_draws, not the library's own generator): the reset() state (set 1) and each
     post-reset state (sets 2, 3); the C oracle replays every step between, bit for bit: the done
-    step's reward and done on the pre-reset state, the post-reset observation, the final state."""
+    step's reward and done on the pre-reset state, the post-reset observation, the final state.
+    Also at configs 2 and 4's shapes (65,536 x 10, 16,384 x 64: other draw-chunk widths, the
+    N = 64 kernels)."""
     from oracle import mt_reset_draws
-    F, N, T, ms, seed = 1 << 20, 5, 10, 7, 4242
+    T, ms, seed = 10, 7, 4242 + N
     ep = ms + 2
     env = venv.FormationEnv({"num_formation": F, "num_agents_per_formation": N,
                              "goal_in_obs": True}, device=DEV, seed=seed, reset_mode="mt19937",

@@ -8,7 +8,9 @@
 // Same bytes (actions 8 B read, obs 32 + reward 4 + done 1 B written per agent-step), no
 // arithmetic, whole float4 runs, plain and non-temporal stores.  Config 3's shape by default.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/plane_order_ubench tools/plane_order_ubench.hip
-//   tools/plane_order_ubench [A] [T]       -> one JSON line per variant
+//   slice_split  slice order as S back-to-back launches over consecutive chunk ranges
+//                (reported as grid -S): does a smaller footprint PER LAUNCH help?
+//   tools/plane_order_ubench [A] [T]       -> one JSON line per variant (SPLIT_ONLY=1: no plane)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -50,8 +52,8 @@ __device__ __forceinline__ void chunk_step(const float4 *__restrict__ act, float
 
 template <bool NT>
 __global__ __launch_bounds__(256) void k_slice(const float4 *act, float4 *obs, float4 *rew,
-                                               float4 *done, int64_t A, int T) {
-    const int64_t c0 = (int64_t)blockIdx.x * CH;
+                                               float4 *done, int64_t A, int T, int64_t b0 = 0) {
+    const int64_t c0 = ((int64_t)blockIdx.x + b0) * CH;
     for (int k = 0; k < T; ++k) chunk_step<NT>(act, obs, rew, done, A, k, c0);
 }
 
@@ -87,14 +89,30 @@ int main(int argc, char **argv) {
         bool nt;
     };
     std::vector<V> vs;
+    const bool split_only = std::getenv("SPLIT_ONLY") != nullptr;
     for (bool nt : {false, true}) {
         vs.push_back({"slice", 0, nt});
-        for (int g : {256, 512, 768, 1024, 1536, 2048}) vs.push_back({"plane", g, nt});
+        if (!split_only)
+            for (int g : {256, 512, 768, 1024, 1536, 2048}) vs.push_back({"plane", g, nt});
+        // slice order in S back-to-back launches over consecutive chunk ranges (grid = -S)
+        for (int S : {2, 4, 8}) vs.push_back({"slice_split", -S, nt});
     }
     for (int round = 0; round < 2; ++round)
         for (const V &v : vs) {
             auto launch = [&] {
-                if (v.grid == 0) {
+                if (v.grid < 0) {
+                    const int S = -v.grid;
+                    const int64_t per = nchunk / S;
+                    for (int k = 0; k < S; ++k) {
+                        const int64_t b0 = k * per, nb = k + 1 < S ? per : nchunk - b0;
+                        if (v.nt)
+                            hipLaunchKernelGGL(k_slice<true>, dim3((unsigned)nb), dim3(256), 0, 0,
+                                               act, obs, rew, done, A, T, b0);
+                        else
+                            hipLaunchKernelGGL(k_slice<false>, dim3((unsigned)nb), dim3(256), 0,
+                                               0, act, obs, rew, done, A, T, b0);
+                    }
+                } else if (v.grid == 0) {
                     if (v.nt)
                         hipLaunchKernelGGL(k_slice<true>, dim3((unsigned)nchunk), dim3(256), 0, 0,
                                            act, obs, rew, done, A, T);
@@ -125,7 +143,8 @@ int main(int argc, char **argv) {
             const double med = ms[ms.size() / 2];
             std::printf("{\"round\": %d, \"order\": \"%s\", \"grid\": %d, \"nt\": %d, \"A\": %lld, "
                         "\"T\": %d, \"ms\": %.4f, \"tb_s\": %.3f}\n",
-                        round, v.name, v.grid ? v.grid : (int)nchunk, v.nt ? 1 : 0, (long long)A,
+                        round, v.name, v.grid > 0 ? v.grid : (v.grid < 0 ? v.grid : (int)nchunk),
+                        v.nt ? 1 : 0, (long long)A,
                         T, med, bytes / (med * 1e-3) / 1e12);
             std::fflush(stdout);
         }
