@@ -154,16 +154,58 @@ size_t draw_scratch_words(int64_t N, int64_t count) {
 // (an L2-resident buffer, `u`, at least draw_scratch_words(N, count) words): a chunk's draws in
 // one fill, then its formations in one pass.  Allocates nothing, so it cannot throw: the
 // draw-ahead thread runs it.
+// Formations [fbase, fbase + count) of the arrays px / py / gx / gy (and their tags) are drawn;
+// the stream must stand at formation fbase's first draw.
 void draw_formations(Mt19937 &mt, int64_t N, int64_t count, uint32_t *u, float *px, float *py,
                      float *gx, float *gy, uint32_t gen = 0, uint32_t *at = nullptr,
-                     uint32_t *gt = nullptr) {
+                     uint32_t *gt = nullptr, int64_t fbase = 0) {
     const int64_t per = 2 * N + 2;
     const int64_t chunk = std::max<int64_t>(1, 49152 / per);
     for (int64_t f0 = 0; f0 < count; f0 += chunk) {
         const int64_t cnt = std::min<int64_t>(chunk, count - f0);
         mt.fill(u, (size_t)(cnt * per));
-        formations_from_draws(u, f0, cnt, N, px, py, gx, gy, gen, at, gt);
+        formations_from_draws(u, fbase + f0, cnt, N, px, py, gx, gy, gen, at, gt);
     }
+}
+
+// A shard's draw set in up to kDrawParts parts on that many host threads: part p starts from a
+// copy of the stream advanced to its first formation (discard twists whole blocks without
+// tempering them, ~3x cheaper per word than a draw), so a config-3 set (12.6M draws) takes a
+// third of the single-thread time; the bits are the single-thread ones.  Sets under
+// kDrawSplitMin draws run on one thread.
+constexpr int kDrawParts = 4;
+constexpr int64_t kDrawSplitMin = (int64_t)1 << 20;
+int draw_parts(int64_t N, int64_t F) { return (2 * N + 2) * F >= kDrawSplitMin ? kDrawParts : 1; }
+
+// Formations [0, F) from the stream's current position, in draw_parts(N, F) parts (chunk buffer
+// of part p at bufs + p * words, words >= draw_scratch_words(N, ceil(F / parts))); leaves mt at
+// formation F's first draw.  Allocates nothing; a thread that cannot be started runs its part on
+// the calling thread.
+void draw_formations_par(Mt19937 &mt, int64_t N, int64_t F, uint32_t *bufs, size_t words,
+                         float *px, float *py, float *gx, float *gy, uint32_t gen = 0,
+                         uint32_t *at = nullptr, uint32_t *gt = nullptr) {
+    const uint64_t per = 2ull * (uint64_t)N + 2ull;
+    const int P = draw_parts(N, F);
+    auto b = [&](int p) { return F * p / P; };  // part p: formations [b(p), b(p + 1))
+    auto part = [&](int p, Mt19937 &m) {
+        draw_formations(m, N, b(p + 1) - b(p), bufs + (size_t)p * words, px, py, gx, gy, gen, at,
+                        gt, b(p));
+    };
+    Mt19937 ms[kDrawParts];
+    std::thread th[kDrawParts];
+    for (int p = 1; p < P; ++p) {
+        ms[p] = mt;
+        ms[p].discard(per * (uint64_t)b(p));
+        try {
+            th[p] = std::thread([&part, &ms, p]() { part(p, ms[p]); });
+        } catch (...) {
+            part(p, ms[p]);
+        }
+    }
+    part(0, mt);
+    for (int p = 1; p < P; ++p)
+        if (th[p].joinable()) th[p].join();
+    if (P > 1) mt = ms[P - 1];  // the last part's stream ends at formation F
 }
 
 // Device frees the runtime refused because a stream capture was under way (a hipFree inside a
@@ -312,7 +354,7 @@ struct fenv {
     int64_t A = 0;
     fenvk::DevState s{};
     // MT19937 reset sets, double-buffered: slot k of `pend` (device) and of `hpend` (pinned,
-    // coherent host memory, read by the staging kernel through `hpend_dev`) each hold one set,
+    // coherent host memory, copied by DMA on the staging stream `cs`) each hold one set,
     // px[A] py[A] gx[F] gy[F].  `rd` is the slot the next reset event reads; a refill writes the
     // other slot, so it never touches a set a queued launch may still read, and the host only
     // rewrites a host slot whose copy (two refills back) has finished.
@@ -343,7 +385,12 @@ struct fenv {
     std::thread ahead;
     // draw_set's chunk buffer, sized at fenv_create: the thread's body allocates nothing, so no
     // std::bad_alloc can escape it (an exception leaving a std::thread calls std::terminate)
-    std::vector<uint32_t> draw_buf;
+    std::vector<uint32_t> draw_buf;  // draw_parts(N, F) chunk buffers, back to back
+    size_t draw_buf_words = 0;        // words per part
+    // the staging copies run on this stream (SDMA, hipMemcpyAsync from the pinned host slot), so
+    // a refill overlaps the episode's launches instead of queueing 1.4 ms of PCIe-bound copy in
+    // front of them; consumers wait for pend_ev, the copy waits for the slot's previous reader
+    hipStream_t cs = nullptr;
     int ahead_slot = -1;     // host slot the thread is drawing into (-1: none)
     uint32_t ahead_gen = 0;  // the generation it is drawing
 
@@ -384,8 +431,8 @@ struct fenv {
         mt.discard(per * (uint64_t)c.f0);
         float *hp = hpend + off;
         uint32_t *at = reinterpret_cast<uint32_t *>(hp + 2 * A + 2 * c.F);
-        draw_formations(mt, c.N, c.F, draw_buf.data(), hp, hp + A, hp + 2 * A, hp + 2 * A + c.F,
-                        gen, at, at + A);
+        draw_formations_par(mt, c.N, c.F, draw_buf.data(), draw_buf_words, hp, hp + A, hp + 2 * A,
+                            hp + 2 * A + c.F, gen, at, at + A);
         mt.discard(per * (uint64_t)(total - c.f0 - c.F));
     }
 
@@ -417,15 +464,18 @@ struct fenv {
         }
         ahead_slot = -1;
         const size_t off = (size_t)w * pend_stride();
-        // the slot's previous reader (the launch that consumed it, on whatever stream) first
-        if (used_ev_recorded[w]) FENV_HIP(hipStreamWaitEvent(st, used_ev[w], 0));
+        // the copy runs on the handle's staging stream, after the slot's previous reader (the
+        // launch that consumed it, on whatever stream)
+        if (used_ev_recorded[w]) FENV_HIP(hipStreamWaitEvent(cs, used_ev[w], 0));
         int32_t mode = 0;
         if (g_stage_n.load() > 0 && g_stage_n.fetch_sub(1) > 0) mode = g_stage_mode.load();
+        if (mode == 1)  // test hook: the copy starts ~0.35 ms late (a sleeping kernel ahead of it)
+            FENV_HIP(fenvk::launch_stage_copy(pend + off, hpend_dev + off, 0, 100, cs));
         if (mode != 2)
-            FENV_HIP(fenvk::launch_stage_copy(pend + off, hpend_dev + off,
-                                              (int64_t)pend_floats(), mode == 1 ? 100 : 0, st));
+            FENV_HIP(hipMemcpyAsync(pend + off, hpend + off, pend_floats() * sizeof(float),
+                                    hipMemcpyHostToDevice, cs));
         slot_gen[w] = gen;
-        FENV_HIP(hipEventRecord(pend_ev[w], st));
+        FENV_HIP(hipEventRecord(pend_ev[w], cs));
         pend_ev_recorded[w] = true;
         rd = w;
         // draw ahead into host slot w ^ 1 once its own copy (queued at the previous refill) has
@@ -565,8 +615,12 @@ int fenv_create(fenv_t **out, int32_t device, int64_t num_formation, int32_t num
             if (he == hipSuccess) he = hipEventCreateWithFlags(&e->used_ev[k], hipEventDisableTiming);
             if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipEventCreate failed"));
         }
+        he = hipStreamCreateWithFlags(&e->cs, hipStreamNonBlocking);
+        if (he != hipSuccess) return cleanup(fail(FENV_EHIP, "hipStreamCreate(staging) failed"));
         try {
-            e->draw_buf.resize(draw_scratch_words(num_agents, num_formation));
+            const int P = draw_parts(num_agents, num_formation);
+            e->draw_buf_words = draw_scratch_words(num_agents, (num_formation + P - 1) / P);
+            e->draw_buf.resize(e->draw_buf_words * (size_t)P);
         } catch (const std::bad_alloc &) {
             return cleanup(fail(FENV_ENOMEM, "draw buffer allocation failed"));
         }
@@ -604,6 +658,10 @@ int fenv_destroy(fenv_t *e) {
     drain_graveyard();
     for (int k = 0; k < 2; ++k)
         if (e->pend_ev_recorded[k]) (void)hipEventSynchronize(e->pend_ev[k]);
+    if (e->cs) {
+        (void)hipStreamSynchronize(e->cs);
+        (void)hipStreamDestroy(e->cs);
+    }
     free_dev(e->device, e->s.px);
     free_dev(e->device, e->pend);
     pinned_give(e->device, e->hpend, e->hpend_dev);
@@ -739,6 +797,10 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
         e->advance_t(L);
         if (event) {
             int rc = e->gen_pending(st);
+            // the call's next launch reads the set just staged: its copy runs on the staging
+            // stream, so the launch stream waits for it (tools/job_r5_e.sh caught the missing
+            // wait with the delayed-copy test hook)
+            if (!rc && k0 + L < T) rc = e->wait_pending(st);
             if (rc) return rc;
         }
         k0 += L;
@@ -874,8 +936,10 @@ int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64
         skip_sets < 0 || (count > 0 && (!px || !py || !gx || !gy)))
         return fail(FENV_EINVAL, "fenv_host_reset_draws: bad arguments");
     std::vector<uint32_t> u;
+    const int P = draw_parts(num_agents, count);
+    const size_t words = draw_scratch_words(num_agents, (count + P - 1) / P);
     try {
-        u.resize(draw_scratch_words(num_agents, count));
+        u.resize(words * (size_t)P);
     } catch (const std::bad_alloc &) {
         return fail(FENV_ENOMEM, "fenv_host_reset_draws: out of host memory");
     }
@@ -883,7 +947,7 @@ int fenv_host_reset_draws(uint32_t seed, int64_t skip_sets, int64_t total, int64
     mt.seed(seed);
     const uint64_t per = 2ull * (uint64_t)num_agents + 2ull;
     mt.discard(per * ((uint64_t)skip_sets * (uint64_t)total + (uint64_t)first));
-    draw_formations(mt, num_agents, count, u.data(), px, py, gx, gy);
+    draw_formations_par(mt, num_agents, count, u.data(), words, px, py, gx, gy);
     return FENV_OK;
 }
 

@@ -49,7 +49,11 @@ def test_desired_neighbor_dist(flib, N):
                                                       (1, 9, 4, 5, 3),
                                                       # discards of many whole 624-word blocks
                                                       # from every offset in a block
-                                                      (5, 2000, 700, 300, 2), (7, 501, 13, 488, 5)])
+                                                      (5, 2000, 700, 300, 2), (7, 501, 13, 488, 5),
+                                                      # >= 2^20 draws: drawn in 4 parts on 4
+                                                      # threads (fenv_api.cpp draw_formations_par)
+                                                      (5, 90000, 0, 90000, 1),
+                                                      (10, 60001, 3001, 50003, 0)])
 def test_host_reset_draws_match_torch_stream(flib, N, total, first, count, skip):
     """Draw set `skip` of the global stream, restricted to formations [first, first+count),
     equals torch.rand after torch.manual_seed (the reference's RNG, simulate.py:133-143)."""
