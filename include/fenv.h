@@ -92,9 +92,10 @@ int fenv_destroy(fenv_t *env);
 int fenv_status(const fenv_t *env);
 
 /* Test hooks of the MT19937 staging (host only).  The next n_refills staging copies, of any
- * handle, run in `mode`: 1 = the copy kernel sleeps ~0.35 ms first (a launch that were not
- * ordered behind its refill would read the slot's old set); 2 = the copy is skipped (the slot
- * keeps its old set: the tag check must fire).  mode 0 / n_refills 0 turns the hook off. */
+ * handle, run in `mode`: 1 = the copy (a DMA on the handle's staging stream) starts ~0.35 ms
+ * late, behind a sleeping kernel (a launch that were not ordered behind its refill would read the
+ * slot's old set); 2 = the copy is skipped (the slot keeps its old set: the tag check must fire).
+ * mode 0 / n_refills 0 turns the hook off. */
 void fenv_test_stage_hook(int32_t mode, int32_t n_refills);
 
 /* Bytes of pinned staging buffers cached for reuse on `device` (bounded at 512 MiB per device;

@@ -196,8 +196,9 @@ def test_view_touches_only_its_formation(venv):
 
 
 def test_mt_reset_staging_across_streams_and_churn(venv):
-    """The MT19937 reset sets are staged into two slots by a copy kernel on the launch stream
-    (DESIGN.md §9): many reset events inside one rollout call (the slot flips at each), launches
+    """The MT19937 reset sets are staged into two slots by a DMA on the handle's own stream,
+    ordered by events: many reset events inside one rollout call (the slot flips
+    at each, and each next launch waits for the set staged at the last), launches
     alternating between two streams (ordered only by stream waits), and staging buffers taken
     back from the process pool by envs of other sizes -- every reward, obs and done bit-exact
     against the C oracle."""
@@ -276,7 +277,7 @@ def _mt_run(venv, F, N, seed, T_calls, hook=None, flib=None, streams=False):
 
 def test_mt_staging_ordering_with_delayed_copies(venv, flib):
     """every staging copy of the run is delayed (fenv_test_stage_hook mode 1:
-    each workgroup of k_stage_copy sleeps ~0.35 ms before copying), so a launch that was not
+    each staging DMA starts behind a kernel sleeping ~0.35 ms), so a launch that was not
     ordered behind its refill -- same stream, or another stream through the events -- would read
     the slot's previous set.  Results stay bit-exact against the C oracle and the tag check stays
     silent: the consumers wait for the copies."""
