@@ -759,8 +759,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         torch.distributed.barrier()
     kern_total_ms = evs[0].elapsed_time(evs[1])
     ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
-    # the same byte mix over the first 4 planes only: a 1 GB reuse footprint instead of 2.46 GB
-    # (the launch's own footprint is what separates the two)
+    # the same byte mix over the first 4 planes only: its 0.17 GB of actions stay in the 256 MB
+    # Infinity Cache from one k_mix launch to the next, so this is NOT an HBM ceiling -- it shows
+    # what the launch's re-read actions cost it (profiles/r5_footprint_ubench.txt)
     ceiling_small = hbm_ceiling(acts[0], obs, rew, done, A, min(T, 4), D, main_s)
     elapsed = pdist.max_over_ranks(elapsed, dev)
     kern_total_ms = pdist.max_over_ranks(kern_total_ms, dev)
@@ -836,8 +837,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 ceiling["small_footprint"] = {
                     "achieved": ceiling_small["achieved"], "steps": ceiling_small["steps"],
                     "frac_of_spec": ceiling_small["achieved"] / HBM_PEAK_GBS,
-                    "note": "k_mix over the first planes only (~1 GB rewritten per launch): what "
-                            "the same byte mix reaches when the footprint is small"}
+                    "note": "k_mix over the first 4 planes only: its 0.17 GB of re-read actions "
+                            "stay in the 256 MB Infinity Cache across launches, so this is the "
+                            "mix with its reads served from the cache, not an HBM ceiling"}
             out["roofline"]["same_box_ceiling"] = ceiling
         if not args.no_stats:
             t = tot.cpu().tolist()

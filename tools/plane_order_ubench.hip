@@ -10,16 +10,19 @@
 //   hipcc --offload-arch=gfx950 -O3 -o tools/plane_order_ubench tools/plane_order_ubench.hip
 //   slice_split  slice order as S back-to-back launches over consecutive chunk ranges
 //                (reported as grid -S): does a smaller footprint PER LAUNCH help?
-//   tools/plane_order_ubench [A] [T]       -> one JSON line per variant (SPLIT_ONLY=1: no plane)
+//   tools/plane_order_ubench [A] [T]       -> one JSON line per variant (SPLIT_ONLY=1: no plane;
+//                                             NOACT=1: no action reads; ALLOC=contig|one)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 constexpr int CH = 1024;  // agents per chunk (one workgroup of 256 threads, 4 agents each)
+__constant__ int act_stride0;  // 1: NOACT (set from the host with hipMemcpyToSymbol)
 
 template <bool NT>
 __device__ __forceinline__ void st(float4 *p, float4 v) {
@@ -40,7 +43,14 @@ __device__ __forceinline__ void chunk_step(const float4 *__restrict__ act, float
                                            int64_t A, int k, int64_t c0) {
     const int tid = threadIdx.x;
     const float4 *a = act + ((int64_t)k * A * 8 + c0 * 8) / 16;
-    const float4 a0 = a[tid], a1 = a[tid + 256];
+    float4 a0, a1;
+    if (act_stride0) {  // NOACT: no action reads (a write-only mix), values from the indices
+        a0 = make_float4((float)tid, (float)k, 1.f, 2.f);
+        a1 = make_float4((float)c0, 0.5f, 3.f, (float)tid);
+    } else {
+        a0 = a[tid];
+        a1 = a[tid + 256];
+    }
     const float s = a0.x + a1.w;
     float4 *o = obs + ((int64_t)k * A * 32 + c0 * 32) / 16;
 #pragma unroll
@@ -73,12 +83,33 @@ int main(int argc, char **argv) {
     if (A % CH) return 2;
     const int64_t nchunk = A / CH;
     float4 *act, *obs, *rew, *done;
-    if (hipMalloc(&act, (size_t)T * A * 8) != hipSuccess ||
-        hipMalloc(&obs, (size_t)T * A * 32) != hipSuccess ||
-        hipMalloc(&rew, (size_t)T * A * 4) != hipSuccess ||
-        hipMalloc(&done, (size_t)T * A) != hipSuccess)
+    // ALLOC=contig: hipExtMallocWithFlags(hipDeviceMallocContiguous) (physically contiguous, so
+    // the page tables can use large fragments); ALLOC=one: the four streams carved from one
+    // hipMalloc; default: one hipMalloc each
+    const char *al = std::getenv("ALLOC");
+    const std::string mode = al ? al : "";
+    auto alloc = [&](float4 **p, size_t b) {
+        if (mode == "contig")
+            return hipExtMallocWithFlags(reinterpret_cast<void **>(p), b,
+                                         hipDeviceMallocContiguous);
+        return hipMalloc(p, b);
+    };
+    if (mode == "one") {
+        char *base = nullptr;
+        const size_t b0 = (size_t)T * A * 8, b1 = (size_t)T * A * 32, b2 = (size_t)T * A * 4;
+        if (hipMalloc(&base, b0 + b1 + b2 + (size_t)T * A) != hipSuccess) return 3;
+        act = reinterpret_cast<float4 *>(base);
+        obs = reinterpret_cast<float4 *>(base + b0);
+        rew = reinterpret_cast<float4 *>(base + b0 + b1);
+        done = reinterpret_cast<float4 *>(base + b0 + b1 + b2);
+    } else if (alloc(&act, (size_t)T * A * 8) != hipSuccess ||
+               alloc(&obs, (size_t)T * A * 32) != hipSuccess ||
+               alloc(&rew, (size_t)T * A * 4) != hipSuccess ||
+               alloc(&done, (size_t)T * A) != hipSuccess)
         return 3;
     (void)hipMemset(act, 0, (size_t)T * A * 8);
+    const int noact = std::getenv("NOACT") ? 1 : 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(act_stride0), &noact, sizeof(int)) != hipSuccess) return 5;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
