@@ -11,7 +11,8 @@
 //   slice_split  slice order as S back-to-back launches over consecutive chunk ranges
 //                (reported as grid -S): does a smaller footprint PER LAUNCH help?
 //   tools/plane_order_ubench [A] [T]       -> one JSON line per variant (SPLIT_ONLY=1: no plane;
-//                                             NOACT=1: no action reads; ALLOC=contig|one)
+//                                             NOACT=1: no action reads; NTLOAD=1: non-temporal
+//                                             action loads; ALLOC=contig|one)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,7 +23,7 @@
 #include <vector>
 
 constexpr int CH = 1024;  // agents per chunk (one workgroup of 256 threads, 4 agents each)
-__constant__ int act_stride0;  // 1: NOACT (set from the host with hipMemcpyToSymbol)
+__constant__ int act_stride0;  // 1: NOACT, 2: NTLOAD (set from the host, hipMemcpyToSymbol)
 
 template <bool NT>
 __device__ __forceinline__ void st(float4 *p, float4 v) {
@@ -44,9 +45,15 @@ __device__ __forceinline__ void chunk_step(const float4 *__restrict__ act, float
     const int tid = threadIdx.x;
     const float4 *a = act + ((int64_t)k * A * 8 + c0 * 8) / 16;
     float4 a0, a1;
-    if (act_stride0) {  // NOACT: no action reads (a write-only mix), values from the indices
+    if (act_stride0 == 1) {  // NOACT: no action reads (a write-only mix), values from the indices
         a0 = make_float4((float)tid, (float)k, 1.f, 2.f);
         a1 = make_float4((float)c0, 0.5f, 3.f, (float)tid);
+    } else if (act_stride0 == 2) {  // NTLOAD: non-temporal action loads
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 *av = reinterpret_cast<const f4 *>(a);
+        const f4 x0 = __builtin_nontemporal_load(av + tid), x1 = __builtin_nontemporal_load(av + tid + 256);
+        a0 = make_float4(x0.x, x0.y, x0.z, x0.w);
+        a1 = make_float4(x1.x, x1.y, x1.z, x1.w);
     } else {
         a0 = a[tid];
         a1 = a[tid + 256];
@@ -108,7 +115,7 @@ int main(int argc, char **argv) {
                alloc(&done, (size_t)T * A) != hipSuccess)
         return 3;
     (void)hipMemset(act, 0, (size_t)T * A * 8);
-    const int noact = std::getenv("NOACT") ? 1 : 0;
+    const int noact = std::getenv("NOACT") ? 1 : (std::getenv("NTLOAD") ? 2 : 0);
     if (hipMemcpyToSymbol(HIP_SYMBOL(act_stride0), &noact, sizeof(int)) != hipSuccess) return 5;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
