@@ -21,7 +21,7 @@ order, of the ranks' j-th row sets -- to summation order (tests/test_distributed
 shards: M = ceil(max n_r / b_local) minibatches per epoch on every rank (the same collective
 count everywhere); a rank whose rows ran out contributes a zero gradient.
 
-Cost model: the replicated path (ppo.py) all-gathers every sample once per update
+Cost model (docs/design_history_r1_r4.md §6): the replicated path (ppo.py) all-gathers every sample once per update
 and runs all n / batch_size x n_epochs minibatches on every rank; this path moves 38.7 KB per
 minibatch per rank through RCCL and divides the per-rank forward/backward work by G, at the price
 of one collective per minibatch.  The minibatch sequence is SB3's and stays sequential either way.
