@@ -400,6 +400,17 @@ struct fenv {
         return fenvk::DevPending{pend ? pend + (size_t)rd * pend_stride() : nullptr,
                                  reinterpret_cast<float4 *>(term), lf, err_dev, slot_gen[rd]};
     }
+    // The constants a rollout launch runs with.  In MT19937 mode the formations move in lock-step
+    // and the host knows which launch holds the reset event (rollout_impl's `event`); a launch
+    // without one takes no reset branch, so it runs the Philox instantiation of the same kernel
+    // -- identical code outside that branch, where the MT19937 instantiation's staged-set reads
+    // cost the config-3 launch ~4 % through register allocation (467.9 vs 449.4 us,
+    // profiles/r5_mt_mode/).  Padding lanes that reach a phantom done draw into registers only.
+    fenvk::Consts launch_consts(bool event) const {
+        fenvk::Consts k = c;
+        if (k.reset_mode == FENV_RESET_MT19937 && !event) k.reset_mode = FENV_RESET_PHILOX;
+        return k;
+    }
 
     // A staged set failed the kernels' tag check in an earlier launch (DevPending): the state
     // may hold wrong draws, so every later call on the handle fails.
@@ -791,7 +802,7 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
             if (g.out) g.out += k0 * A * 2;
         }
         FENV_HIP(fenvk::launch_rollout(
-            e->c, e->s, e->pending(), (int32_t)L, (int32_t)D, act ? act + k0 * A * 2 : nullptr,
+            e->launch_consts(event), e->s, e->pending(), (int32_t)L, (int32_t)D, act ? act + k0 * A * 2 : nullptr,
             obs ? obs + k0 * A * D : nullptr, rew ? rew + k0 * A : nullptr,
             done ? done + k0 * A : nullptr, partial, k0 > 0, nt, st, gen ? &g : nullptr));
         e->advance_t(L);
@@ -1028,7 +1039,7 @@ int fenv_policy_rollout(fenv_t *e, const float *params, int32_t T, uint64_t seed
         }
         g.b.last_value = e->lv_scratch;
     }
-    FENV_HIP(fenvk::launch_policy_rollout(e->c, e->s, e->pending(), e->D, g, st));
+    FENV_HIP(fenvk::launch_policy_rollout(e->launch_consts(event), e->s, e->pending(), e->D, g, st));
     e->advance_t(T);
     if (event) {
         int rc = e->gen_pending(st);
