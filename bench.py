@@ -355,9 +355,9 @@ def random_action_bench(pkgname: str, dev, formations: int, agents: int, launche
 
 def numpy_face_bench(pkgname: str, dev, formations: int, agents: int, steps: int) -> dict:
     """The PCIe-inclusive rate: the reference's own interface, ``FormationEnv.step(np.ndarray)``
-    (vectorized_env.py:68-82, what SB3's VecEnv loop calls), which copies the actions host ->
-    device and obs / reward / done device -> host through pinned buffers every step.  Never the
-    headline `value` (its inputs are not HBM-resident)."""
+    (vectorized_env.py:68-82, what SB3's VecEnv loop calls): the kernel reads the actions from
+    and writes obs / reward / done to device-mapped host memory, so every step crosses PCIe.
+    Never the headline `value` (its inputs are not HBM-resident)."""
     import numpy as np
     from importlib import import_module
     venv = import_module(pkgname + ".vectorized_env")

@@ -36,8 +36,9 @@ extern "C" {
  *   2  + fenv_abi_version, fenv_get_state_range, fenv_metrics_range, ppo_workspace_bytes,
  *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject
  *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes, fenv_debug_staging (no
- *        signature changed) */
-#define FENV_ABI_VERSION 3
+ *        signature changed)
+ *   4  + fenv_host_alloc, fenv_host_free (no signature changed) */
+#define FENV_ABI_VERSION 4
 int fenv_abi_version(void);
 
 typedef struct fenv fenv_t;
@@ -101,6 +102,18 @@ void fenv_test_stage_hook(int32_t mode, int32_t n_refills);
 /* Bytes of pinned staging buffers cached for reuse on `device` (bounded at 512 MiB per device;
  * a destroyed env's buffer is freed instead when the pool is full). */
 int64_t fenv_pinned_pool_bytes(int32_t device);
+
+/* Host memory the kernels read and write in place (zero-copy): coherent host memory mapped into
+ * the device's address space, *dev its device address.  The host faces of reset / step
+ * (FormationEnv.reset / step with numpy arrays, vectorized_env.py:52-55, 68-82) pass the `dev`
+ * addresses of such a block as act / obs / rew / done to fenv_reset / fenv_step and synchronize the
+ * stream: no DMA copies (config 0, 1,000 x 5: 20.7 us per step against 58.2 us through pinned
+ * mirrors and four hipMemcpyAsync).  Blocks come from the same pooled, bounded pinned cache as the
+ * MT19937 staging sets; `bytes` is rounded up to 256. */
+int fenv_host_alloc(int32_t device, int64_t bytes, void **host, void **dev);
+/* Returns a fenv_host_alloc block (host address) to `device`'s pool; NULL is a no-op.  The caller
+ * makes sure no queued launch still reads or writes it. */
+int fenv_host_free(int32_t device, void *host);
 
 /* Diagnostic (synchronous): info_host[0..9] = {slot the next reset reads, generation of slot 0,
  * of slot 1, floats per staged set, error words 0..2, next generation, device address of the

@@ -9,6 +9,9 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import weakref
+
+import numpy as np
 
 import torch  # noqa: F401  (must precede loading libfenv.so: shared HIP runtime)
 
@@ -70,6 +73,8 @@ SIGNATURES = {
     "fenv_status": (_I32, [_P]),
     "fenv_test_stage_hook": (None, [_I32, _I32]),
     "fenv_pinned_pool_bytes": (_I64, [_I32]),
+    "fenv_host_alloc": (_I32, [_I32, _I64, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "fenv_host_free": (_I32, [_I32, _P]),
     "fenv_debug_staging": (_I32, [_P, _I32, _P, _P]),
     "fenv_last_error": (ctypes.c_char_p, []),
 }
@@ -176,3 +181,38 @@ def require_device(device=None) -> torch.device:
     if d.type != "cuda":
         raise ValueError(f"FormationEnv device must be a HIP device, got {d}")
     return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
+
+
+def _host_free(device: int, host: int) -> None:
+    if _lib is not None:
+        _lib.fenv_host_free(device, ctypes.c_void_p(host))
+
+
+class HostBlock:
+    """Numpy arrays in one block of coherent, device-mapped host memory (``fenv_host_alloc``): the
+    kernels read and write them in place, so the numpy faces of reset / step need no DMA copies.
+    ``fields`` is [(name, numpy dtype, shape)]; each field is an attribute (the numpy array,
+    256-B aligned in the block) and ``dev(name)`` its device address.  The block goes back to the
+    library's pool when the last array viewing it is gone, so arrays a caller kept stay valid
+    after the env that filled them is released."""
+
+    def __init__(self, device: torch.device, fields):
+        offs, total = {}, 0
+        for name, dt, shape in fields:
+            offs[name] = total
+            total += (int(np.prod(shape)) * np.dtype(dt).itemsize + 255) // 256 * 256
+        h, d = _P(), _P()
+        check(lib().fenv_host_alloc(device.index, max(total, 256), ctypes.byref(h),
+                                    ctypes.byref(d)), "fenv_host_alloc")
+        raw = (ctypes.c_uint8 * max(total, 256)).from_address(h.value)
+        # freed with the last view: the arrays below hold `raw` through their base chain
+        weakref.finalize(raw, _host_free, device.index, h.value)
+        base = np.ctypeslib.as_array(raw)
+        self._dev = {}
+        for name, dt, shape in fields:
+            n = int(np.prod(shape)) * np.dtype(dt).itemsize
+            setattr(self, name, base[offs[name]:offs[name] + n].view(dt).reshape(shape))
+            self._dev[name] = ctypes.c_void_p(d.value + offs[name])
+
+    def dev(self, name: str) -> ctypes.c_void_p:
+        return self._dev[name]

@@ -279,8 +279,9 @@ hipError_t pinned_take(int32_t device, size_t bytes, float **host, float **dev) 
         (void)hipHostFree(h);
         return he;
     }
-    // the pool entry records its capacity in the word before the buffer
+    // the pool entry records its capacity and device address in the header before the buffer
     *reinterpret_cast<size_t *>(h) = bytes;
+    reinterpret_cast<void **>(h)[1] = d;
     *host = reinterpret_cast<float *>(reinterpret_cast<char *>(h) + 256);
     *dev = reinterpret_cast<float *>(reinterpret_cast<char *>(d) + 256);
     return hipSuccess;
@@ -300,6 +301,14 @@ void pinned_give(int32_t device, float *host, float *dev) {
     }
     free_host(device, base);
 }
+// Blocks handed out by fenv_host_alloc and not yet freed (device, host address): fenv_host_free
+// of anything else returns FENV_EINVAL without reading it.
+std::mutex g_host_blocks_mu;
+std::map<void *, int32_t> &host_blocks() {
+    static auto *m = new std::map<void *, int32_t>();  // never destroyed: usable from finalizers
+    return *m;
+}
+
 size_t pinned_cached(int32_t device) {
     std::lock_guard<std::mutex> lk(pinned_pool().mu);
     auto it = pinned_pool().cached.find(device);
@@ -714,6 +723,43 @@ void fenv_test_stage_hook(int32_t mode, int32_t n_refills) {
 }
 
 int64_t fenv_pinned_pool_bytes(int32_t device) { return (int64_t)pinned_cached(device); }
+
+int fenv_host_alloc(int32_t device, int64_t bytes, void **host, void **dev) {
+    if (!host || !dev || bytes < 0) return fail(FENV_EINVAL, "fenv_host_alloc: bad arguments");
+    int count = 0;
+    FENV_HIP(hipGetDeviceCount(&count));
+    if (device < 0 || device >= count) return fail(FENV_EINVAL, "fenv_host_alloc: no such device");
+    drain_graveyard();
+    float *h = nullptr, *d = nullptr;
+    // the pool's 256-B header precedes the block; blocks are whole 256-B units
+    const size_t want = ((size_t)bytes + 255) / 256 * 256 + 256;
+    if (pinned_take(device, want, &h, &d) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FENV_ENOMEM, "fenv_host_alloc: hipHostMalloc failed");
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_host_blocks_mu);
+        host_blocks()[h] = device;
+    }
+    *host = h;
+    *dev = d;
+    return FENV_OK;
+}
+
+int fenv_host_free(int32_t device, void *host) {
+    if (!host) return FENV_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_host_blocks_mu);
+        auto it = host_blocks().find(host);
+        if (it == host_blocks().end() || it->second != device)
+            return fail(FENV_EINVAL, "fenv_host_free: not a live fenv_host_alloc block of this device");
+        host_blocks().erase(it);
+    }
+    void *d = reinterpret_cast<void **>(static_cast<char *>(host) - 256)[1];
+    pinned_give(device, static_cast<float *>(host),
+                reinterpret_cast<float *>(static_cast<char *>(d) + 256));
+    return FENV_OK;
+}
 
 int fenv_debug_staging(fenv_t *e, int32_t which, float *out_host, int64_t *info_host) {
     if (!e || !info_host) return fail(FENV_EINVAL, "fenv_debug_staging: NULL argument");

@@ -155,8 +155,7 @@ class FormationEnv(_BASE):
         self.obs_dev = torch.zeros((A, D), dtype=torch.float32, device=dev)
         self.rew_dev = torch.zeros(A, dtype=torch.float32, device=dev)
         self.done_dev = torch.zeros(A, dtype=torch.bool, device=dev)
-        self._act_dev = torch.zeros((A, 2), dtype=torch.float32, device=dev)
-        self._host = None  # pinned host mirrors, created on first numpy call
+        self._host = None  # zero-copy host arrays of the numpy faces, created on first use
         self.infos = _Infos(A)                                # vectorized_env.py:49
         self.formationsim_list = FormationViewList(self, F)  # vectorized_env.py:38
         self._fig = None
@@ -191,7 +190,7 @@ class FormationEnv(_BASE):
                 torch.cuda.current_stream(self.device).synchronize()
                 _lib.destroy_handle(h)
         self._host = None
-        for k in ("obs_dev", "rew_dev", "done_dev", "_act_dev"):
+        for k in ("obs_dev", "rew_dev", "done_dev"):
             if hasattr(self, k):
                 setattr(self, k, None)
 
@@ -215,16 +214,16 @@ class FormationEnv(_BASE):
             except Exception:
                 pass
 
-    def _ensure_host(self):
+    def _ensure_host(self) -> _lib.HostBlock:
+        """The numpy faces' arrays (vectorized_env.py:46-48 obs_buf / reward_buf / done_buf, plus
+        the actions) in device-mapped host memory: the kernels read the actions and write the
+        outputs there directly, so a numpy step is one launch and a synchronize."""
         if self._host is None:
             A, D = self.num_envs, self.obs_dim
-            pin = torch.cuda.is_available()
-            self._host = dict(
-                obs=torch.zeros((A, D), dtype=torch.float32, pin_memory=pin),
-                rew=torch.zeros(A, dtype=torch.float32, pin_memory=pin),
-                done=torch.zeros(A, dtype=torch.bool, pin_memory=pin),
-                act=torch.zeros((A, 2), dtype=torch.float32, pin_memory=pin),
-            )
+            self._host = _lib.HostBlock(self.device, [("act", np.float32, (A, 2)),
+                                                      ("obs", np.float32, (A, D)),
+                                                      ("rew", np.float32, (A,)),
+                                                      ("done", np.bool_, (A,))])
         return self._host
 
     def _make_view(self, i: int) -> FormationView:
@@ -262,41 +261,39 @@ class FormationEnv(_BASE):
 
     # ------------------------------------------------------------------ reference API
     def reset(self) -> np.ndarray:
-        """vectorized_env.py:52-55: reset every formation and return obs [A, D] (numpy)."""
-        self.reset_tensor()
-        return self._to_host_obs()
+        """vectorized_env.py:52-55: reset every formation and return obs [A, D] (numpy, written in
+        place by the kernel; aliases this env's host array like the reference's obs_buf)."""
+        host = self._ensure_host()
+        _lib.check(_lib.lib().fenv_reset(self._h, host.dev("obs"), self._stream()), "fenv_reset")
+        return self._host_result(host).obs
 
     def compute_observations(self) -> np.ndarray:
         """vectorized_env.py:57-66 (numpy view of the current observations)."""
-        self.observe_tensor()
-        return self._to_host_obs()
+        host = self._ensure_host()
+        _lib.check(_lib.lib().fenv_observe(self._h, host.dev("obs"), self._stream()),
+                   "fenv_observe")
+        return self._host_result(host).obs
 
     def step(self, actions):
         """vectorized_env.py:68-82.  ``actions`` [A, 2] in the action space (numpy or tensor).
 
         Returns ``(obs, rewards, dones, infos)`` as numpy arrays that alias this env's host
         buffers (overwritten by the next call, like the reference's ``obs_buf.numpy()``)."""
+        host = self._ensure_host()
         if isinstance(actions, torch.Tensor) and actions.is_cuda:
-            act = actions
+            act = self._check_act(actions, ())
+            act_p = _lib.ptr(act)
         else:
             a = np.asarray(actions, dtype=np.float32)
             if a.shape != (self.num_envs, 2):
                 # simulate.py:79 asserts input_velocity.shape == agents.shape per formation
                 raise AssertionError(f"actions shape {a.shape} != {(self.num_envs, 2)}")
-            host = self._ensure_host()
-            host["act"].numpy()[...] = a
-            self._act_dev.copy_(host["act"], non_blocking=True)
-            act = self._act_dev
-        self.step_tensor(act)
-        host = self._ensure_host()
-        host["obs"].copy_(self.obs_dev, non_blocking=True)
-        host["rew"].copy_(self.rew_dev, non_blocking=True)
-        host["done"].copy_(self.done_dev, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        self.check()
-        if self._fig is not None:
-            self._refresh_fig()
-        return host["obs"].numpy(), host["rew"].numpy(), host["done"].numpy(), self.infos
+            np.copyto(host.act, a)
+            act_p = host.dev("act")
+        _lib.check(_lib.lib().fenv_step(self._h, act_p, host.dev("obs"), host.dev("rew"),
+                                        host.dev("done"), self._stream()), "fenv_step")
+        self._host_result(host)
+        return host.obs, host.rew, host.done, self.infos
 
     def close(self):
         raise NotImplementedError
@@ -323,14 +320,13 @@ class FormationEnv(_BASE):
         raise NotImplementedError
 
     # ------------------------------------------------------------------ device faces
-    def _to_host_obs(self) -> np.ndarray:
-        host = self._ensure_host()
-        host["obs"].copy_(self.obs_dev, non_blocking=True)
+    def _host_result(self, host: _lib.HostBlock) -> _lib.HostBlock:
+        """Wait for the launch that writes the host arrays, then the faces' common tail."""
         torch.cuda.current_stream(self.device).synchronize()
         self.check()
         if self._fig is not None:
             self._refresh_fig()
-        return host["obs"].numpy()
+        return host
 
     def reset_tensor(self) -> torch.Tensor:
         """Reset every formation; returns the device obs buffer [A, D]."""

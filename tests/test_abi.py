@@ -226,6 +226,19 @@ def test_abi_version_matches_header(flib):
     assert flib.lib().ppo_workspace_bytes() >= 16
 
 
+def test_host_free_rejects_foreign_pointers(flib):
+    """fenv_host_free(NULL) is a no-op; a pointer fenv_host_alloc did not hand out (or already
+    took back) is rejected with FENV_EINVAL before anything is read from it (no device needed)."""
+    import ctypes
+    L = flib.lib()
+    assert L.fenv_host_free(0, None) == 0
+    buf = ctypes.create_string_buffer(1024)
+    assert L.fenv_host_free(0, ctypes.cast(ctypes.byref(buf, 512), ctypes.c_void_p)) != 0
+    assert b"fenv_host_alloc" in L.fenv_last_error()
+    h, d = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.fenv_host_alloc(0, -1, ctypes.byref(h), ctypes.byref(d)) != 0
+
+
 def test_destroy_null_and_range_args_fail_cleanly(flib):
     """fenv_destroy(NULL) is a no-op; the range queries reject a NULL handle with an error code
     (no device needed)."""

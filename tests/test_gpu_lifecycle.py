@@ -64,7 +64,7 @@ def test_release_is_deterministic_and_idempotent(venv, flib):
 def test_churn_envs_across_paths_with_gc(venv):
     """Create and drop ~300 envs over the wavefront (N <= 64, incl. the staged and role-split
     kernels), workgroup (64 < N <= 1024) and large-formation (N > 1024) paths, both reset modes,
-    the numpy face (pinned host mirrors) and the device faces, some released explicitly, some
+    the numpy face (device-mapped host arrays) and the device faces, some released explicitly, some
     dropped, some left to the collector, with gc.collect() interleaved; every 25th env is checked
     against the C oracle bit for bit."""
     shapes = [(5, 1), (1, 5), (4096, 5), (60, 64), (3, 100), (2, 1024), (2, 1025), (1, 1300),
@@ -309,6 +309,55 @@ def test_mt_staging_check_fires_on_a_stale_set(venv, flib):
         finally:
             flib.lib().fenv_test_stage_hook(0, 0)
         env.release()
+
+
+def test_numpy_face_zero_copy_arrays(venv, flib):
+    """The numpy faces' arrays live in device-mapped host memory the kernels write in place
+    (fenv_host_alloc): every call returns the same arrays (aliasing, like the reference's
+    obs_buf.numpy()); the done array holds 0 / 1 bytes; a CUDA action tensor drives the same
+    step; arrays a caller kept stay valid after the env is released, and their block goes back
+    to the pool only when the last one is gone.  Host blocks are freed once, and only by their
+    own device."""
+    import ctypes
+    L = flib.lib()
+    F, N = 300, 5
+    A = F * N
+    env = make_env(venv, F, N, seed=3, reset_mode="philox", max_steps=4)
+    twin = make_env(venv, F, N, seed=3, reset_mode="philox", max_steps=4)
+    o0 = env.reset()
+    twin.reset_tensor()
+    assert np.array_equal(o0.view(np.uint32), twin.obs_dev.cpu().numpy().view(np.uint32))
+    for k in range(12):
+        a = synth_actions(3, k, A, 1.3)
+        if k % 3 == 2:  # the CUDA-tensor form of the same face
+            o, r, d, _ = env.step(torch.from_numpy(a).to(DEV))
+        else:
+            o, r, d, _ = env.step(a)
+        to, tr, td = twin.step_tensor(torch.from_numpy(a).to(DEV))
+        assert o is o0 and np.shares_memory(o, o0)
+        assert np.array_equal(o.view(np.uint32), to.cpu().numpy().view(np.uint32)), k
+        assert np.array_equal(r.view(np.uint32), tr.cpu().numpy().view(np.uint32)), k
+        assert np.array_equal(d, td.cpu().numpy()), k
+        assert set(np.unique(d.view(np.uint8)).tolist()) <= {0, 1}
+    assert d.any()  # max_steps 4: resets happened inside the window
+    kept = o.copy()
+    env.release()
+    twin.release()
+    del env
+    gc.collect()
+    assert np.array_equal(o.view(np.uint32), kept.view(np.uint32))  # block still held by `o`
+    before = L.fenv_pinned_pool_bytes(0)
+    del o, o0, r, d
+    gc.collect()
+    # back in the pool (a cached buffer of up to 4x the request may have served it), unless the
+    # pool was already too full to take it
+    blk = 256 + sum((n + 255) // 256 * 256 for n in (A * 8, A * 32, A * 4, A))
+    assert L.fenv_pinned_pool_bytes(0) > before or before > (512 << 20) - 4 * blk
+    h, dv = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.fenv_host_alloc(0, 4096, ctypes.byref(h), ctypes.byref(dv)) == 0 and h.value and dv.value
+    assert L.fenv_host_free(1 if torch.cuda.device_count() > 1 else 99, h) != 0  # other device
+    assert L.fenv_host_free(0, h) == 0
+    assert L.fenv_host_free(0, h) != 0  # freed once
 
 
 def test_pinned_pool_bounded_under_growing_sizes(venv, flib):
