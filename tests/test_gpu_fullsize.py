@@ -386,3 +386,30 @@ def test_mt19937_config3_resets_vs_stream(venv, F, N):
                             ("t", t1, rs[4], fst)):
         assert np.array_equal(bits(v[idx].cpu().numpy()), bits(w)), name
     env.release()
+
+
+@pytest.mark.parametrize("F,N", [(1_048_576, 5), (16_384, 64)])
+def test_numpy_face_full_size_matches_device_face(venv, F, N):
+    """BASELINE configs 3 and 4 through the numpy face, whose kernel reads the actions from and
+    writes obs / reward / done to device-mapped host memory over PCIe (non-temporal stores at
+    this size): bit-identical to the device face on a twin env, step by step, across a reset
+    event (max_steps 2)."""
+    cfg = {"num_formation": F, "num_agents_per_formation": N, "goal_in_obs": True}
+    env = venv.FormationEnv(cfg, device=DEV, seed=5, reset_mode="philox", max_steps=2, log=False)
+    twin = venv.FormationEnv(cfg, device=DEV, seed=5, reset_mode="philox", max_steps=2, log=False)
+    A = F * N
+    o = env.reset()
+    assert np.array_equal(o.view(np.uint32), twin.reset_tensor().cpu().numpy().view(np.uint32))
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dones = 0
+    for k in range(5):
+        a = torch.rand((A, 2), device=DEV, generator=g) * 2.4 - 1.2
+        o, r, d, _ = env.step(a.cpu().numpy())
+        to, tr, td = twin.step_tensor(a)
+        dones += int(d.sum())
+        assert np.array_equal(o.view(np.uint32), to.cpu().numpy().view(np.uint32)), k
+        assert np.array_equal(r.view(np.uint32), tr.cpu().numpy().view(np.uint32)), k
+        assert np.array_equal(d, td.cpu().numpy()), k
+    assert dones == A  # max_steps 2: a 4-step episode, every formation done once in 5 steps
+    env.release()
+    twin.release()
