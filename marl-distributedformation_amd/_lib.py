@@ -183,9 +183,29 @@ def require_device(device=None) -> torch.device:
     return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
 
 
+# live HostBlocks: host address -> (bytes, device address), for device_address()
+_blocks: dict[int, tuple[int, int]] = {}
+
+
 def _host_free(device: int, host: int) -> None:
+    _blocks.pop(host, None)
     if _lib is not None:
         _lib.fenv_host_free(device, ctypes.c_void_p(host))
+
+
+def device_address(a: np.ndarray, align: int = 16) -> ctypes.c_void_p | None:
+    """The device address of a C-contiguous numpy array that lies inside a live HostBlock (e.g.
+    an observation array a FormationEnv's numpy face returned), so a kernel can read it in place;
+    None for any other array, or one not aligned to ``align`` bytes."""
+    if not isinstance(a, np.ndarray) or not a.flags.c_contiguous:
+        return None
+    p = a.ctypes.data
+    if p % align:
+        return None
+    for base, (n, dev) in list(_blocks.items()):
+        if base <= p and p + a.nbytes <= base + n:
+            return ctypes.c_void_p(dev + (p - base))
+    return None
 
 
 class HostBlock:
@@ -207,6 +227,7 @@ class HostBlock:
         raw = (ctypes.c_uint8 * max(total, 256)).from_address(h.value)
         # freed with the last view: the arrays below hold `raw` through their base chain
         weakref.finalize(raw, _host_free, device.index, h.value)
+        _blocks[h.value] = (max(total, 256), d.value)
         base = np.ctypeslib.as_array(raw)
         self._dev = {}
         for name, dt, shape in fields:

@@ -65,6 +65,7 @@ class MlpPolicy:
         assert o == n
         self.reset_parameters(seed, log_std_init)
         self._offset = 0
+        self._host = {}  # predict(): device-mapped host arrays per batch size (_lib.HostBlock)
         self.sample_seed = int(seed)
 
     # ---------------------------------------------------------------- parameters
@@ -158,8 +159,36 @@ class MlpPolicy:
     __call__ = forward
 
     def predict(self, observation, deterministic: bool = True):
-        """SB3 ``predict``: numpy obs [B, D] -> (clipped actions numpy [B, 2], None)."""
-        obs = torch.as_tensor(np.asarray(observation, np.float32)).to(self.device)
-        r = self.forward(obs, deterministic=deterministic)
-        return r["clipped"].cpu().numpy(), None
+        """SB3 ``predict``: numpy obs [B, D] -> (clipped actions numpy [B, 2], None).
+
+        The kernel reads the observations and writes the actions in device-mapped host memory
+        (``_lib.HostBlock``): observations a FormationEnv's numpy face returned are read in place,
+        others are first copied into the policy's block; the actions come back as a new array.
+        Same bits and the same noise offset advance as ``forward(...)["clipped"]``."""
+        if isinstance(observation, torch.Tensor) and observation.is_cuda:
+            return self.forward(observation, deterministic=deterministic)["clipped"].cpu().numpy(), None
+        obs = np.asarray(observation, np.float32)
+        if obs.ndim != 2 or obs.shape[1] != self.obs_dim:
+            raise ValueError(f"obs must be [B, {self.obs_dim}]")
+        B = obs.shape[0]
+        if B == 0:
+            return np.zeros((0, 2), np.float32), None
+        host = self._host.get(B)
+        if host is None:
+            host = _lib.HostBlock(self.device, [("obs", np.float32, (B, self.obs_dim)),
+                                                ("clipped", np.float32, (B, 2))])
+            self._host = {B: host}  # one batch size cached (playback and SB3 loops keep theirs)
+        d_obs = _lib.device_address(obs)
+        if d_obs is None:
+            np.copyto(host.obs, obs)
+            d_obs = host.dev("obs")
+        offset = self._offset
+        self._offset += 1
+        dev = self.device
+        _lib.check(_lib.lib().policy_forward(
+            _lib.ptr(self.flat), self.obs_dim, d_obs, B, 0, None, None, None, None,
+            host.dev("clipped"), int(self.sample_seed) & 0xFFFFFFFFFFFFFFFF, int(offset),
+            int(bool(deterministic)), _lib.current_stream(dev)), "policy_forward")
+        torch.cuda.current_stream(dev).synchronize()
+        return host.clipped.copy(), None
 

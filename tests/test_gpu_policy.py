@@ -141,3 +141,53 @@ def test_batch_beyond_int32_offsets_sampled(pol_mod):
     assert_rel_close(r["mu"][idx], mu, "mu")
     assert_rel_close(r["value"][idx], val, "value")
     assert_rel_close(r["clipped"][idx], mu.clamp(-1, 1), "clipped")
+
+
+def test_predict_zero_copy_matches_forward(pkg, pol_mod):
+    """SB3 ``predict`` (visualize_policy.py:16) runs the kernel on device-mapped host memory: an
+    env's numpy-face observations are read in place, other numpy arrays (plain, strided, sliced
+    to an unaligned start) are copied into the policy's block first, and CUDA tensors go through
+    ``forward``.  Every form returns the bits of ``forward(...)["clipped"]`` at the same noise
+    offset -- deterministic and sampled -- as a fresh array that later calls leave alone."""
+    from importlib import import_module
+    venv = import_module(pkg.__name__ + ".vectorized_env")
+    flib = import_module(pkg.__name__ + "._lib")
+    env = venv.FormationEnv({"num_formation": 40, "num_agents_per_formation": 5,
+                             "goal_in_obs": True}, log=False, device=DEV, seed=2,
+                            reset_mode="philox")
+    pol = pol_mod.MlpPolicy(8, device=DEV, seed=9)
+    randomize(pol, 4)
+    obs = env.reset()
+    assert flib.device_address(obs) is not None          # lives in the env's host block
+    assert flib.device_address(obs.copy()) is None
+    assert flib.device_address(obs[1:]) is not None      # 32-B rows keep 16-B alignment
+    raw = np.zeros(obs.size + 1, np.float32)
+    unaligned = raw[1:].reshape(obs.shape)               # 4-B aligned start: copied first
+    unaligned[...] = obs
+    forms = {"env": obs, "env_rows": obs[40:], "plain": obs.copy(),
+             "strided": np.asfortranarray(obs), "unaligned": unaligned}
+    kept = []
+    for det in (True, False):
+        for name, o in forms.items():
+            off = pol._offset
+            ref = pol.forward(torch.from_numpy(np.ascontiguousarray(o)).to(DEV),
+                              deterministic=det, offset=off)["clipped"].cpu().numpy()
+            pol._offset = off
+            got, st = pol.predict(o, deterministic=det)
+            assert st is None and got.shape == (o.shape[0], 2)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (name, det)
+            assert pol._offset == off + 1
+            kept.append((got, got.copy()))
+    t = torch.from_numpy(obs.copy()).to(DEV)
+    off = pol._offset
+    ref = pol.forward(t, deterministic=True, offset=off)["clipped"].cpu().numpy()
+    pol._offset = off
+    assert np.array_equal(pol.predict(t)[0], ref)
+    # a different batch size replaces the cached block; earlier results are untouched
+    o2, _, _, _ = env.step(np.zeros((200, 2), np.float32))
+    assert pol.predict(o2[:40])[0].shape == (40, 2)
+    for got, snap in kept:
+        assert np.array_equal(got, snap)
+    with pytest.raises(ValueError):
+        pol.predict(np.zeros((4, 6), np.float32))
+    env.release()
