@@ -202,7 +202,7 @@ def device_address(a: np.ndarray, align: int = 16) -> ctypes.c_void_p | None:
     p = a.ctypes.data
     if p % align:
         return None
-    for base, (n, dev) in list(_blocks.items()):
+    for base, (n, dev) in _blocks.copy().items():  # a finalizer may drop a block meanwhile
         if base <= p and p + a.nbytes <= base + n:
             return ctypes.c_void_p(dev + (p - base))
     return None
