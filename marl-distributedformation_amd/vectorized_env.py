@@ -151,7 +151,9 @@ class FormationEnv(_BASE):
         self._npartial = int(L.fenv_partial_count(h))
         A, D, F = self.num_envs, self.obs_dim, self.num_formation
         dev = self.device
-        # device buffers (vectorized_env.py:46-48 obs_buf / reward_buf / done_buf)
+        # the device faces' default outputs (reset_tensor / observe_tensor / step_tensor); the
+        # numpy faces write their own host arrays instead (_ensure_host), so these hold the last
+        # device-face results, not necessarily the last step's
         self.obs_dev = torch.zeros((A, D), dtype=torch.float32, device=dev)
         self.rew_dev = torch.zeros(A, dtype=torch.float32, device=dev)
         self.done_dev = torch.zeros(A, dtype=torch.bool, device=dev)
