@@ -1,8 +1,9 @@
 /* The C ABI (include/fenv.h) driven from plain C, without Python or torch in the process: the
  * way a C / C++ training loop would bind libfenv.so.  A small env (F = 37 formations x N
  * agents, both obs layouts, MT19937 resets every 11 steps) is reset, rolled out in fused chunks
- * that straddle reset events and stepped once more; every observation, reward and done byte and
- * the final state are compared with the CPU oracle (oracle/fenv_oracle.c, test infrastructure).
+ * that straddle reset events, stepped once more, then once through device-mapped host memory
+ * (fenv_host_alloc); every observation, reward and done byte and the final state are compared
+ * with the CPU oracle (oracle/fenv_oracle.c, test infrastructure).
  * Also checks the ABI's error contract (negative code + fenv_last_error) on bad arguments.
  * Built by tests/c_abi/Makefile (from __graft_entry__.build()); run by
  * tests/test_gpu_c_abi.py on the GPU box.  Exit 0 = all bit-exact. */
@@ -101,6 +102,31 @@ static int run(int32_t N, int goal) {
             ok &= same(h_obs + (int64_t)k * A * D, r_obs, sizeof(float) * A * D, "obs", step);
             ok &= same(h_rew + (int64_t)k * A, r_rew, sizeof(float) * A, "reward", step);
             ok &= same(h_done + (int64_t)k * A, r_done, (size_t)A, "done", step);
+        }
+    }
+    /* one more step through device-mapped host memory (fenv_host_alloc): the kernel reads the
+     * actions and writes obs / reward / done in the host block, no copies */
+    if (ok) {
+        const size_t sa = (size_t)A * 8, so = (size_t)A * D * 4, sr = (size_t)A * 4;
+        const size_t oa = 0, oo = (sa + 255) / 256 * 256, orw = oo + (so + 255) / 256 * 256,
+                     od = orw + (sr + 255) / 256 * 256;
+        void *hb = NULL, *db = NULL;
+        ABI(fenv_host_alloc(0, (int64_t)(od + (size_t)A), &hb, &db));
+        char *h = (char *)hb, *d = (char *)db;
+        for (int64_t q = 0; q < A * 2; ++q)
+            ((float *)(h + oa))[q] = (float)((double)(sm64(&s) >> 40) * 0x1.0p-24 * 2.4 - 1.2);
+        ABI(fenv_step(env, (const float *)(d + oa), (float *)(d + oo), (float *)(d + orw),
+                      (uint8_t *)(d + od), NULL));
+        HIP(hipDeviceSynchronize());
+        ++step;
+        orc_env_step(ref, (const float *)(h + oa), r_obs, r_rew, r_done);
+        ok &= same(h + oo, r_obs, so, "host-block obs", step);
+        ok &= same(h + orw, r_rew, sr, "host-block reward", step);
+        ok &= same(h + od, r_done, (size_t)A, "host-block done", step);
+        ABI(fenv_host_free(0, hb));
+        if (fenv_host_free(0, hb) >= 0) {  /* a second free is refused */
+            fprintf(stderr, "fenv_host_free accepted a freed block\n");
+            ok = 0;
         }
     }
     /* final state */
