@@ -258,3 +258,24 @@ def test_destroy_of_unknown_handle_is_refused(flib):
     junk = ctypes.create_string_buffer(b"\xff" * 4096)
     assert L.fenv_destroy(ctypes.cast(junk, ctypes.c_void_p)) == -1
     assert b"not a live handle" in L.fenv_last_error()
+
+
+def test_device_address_lookup(flib):
+    """``_lib.device_address``: an array inside a registered host block maps to the block's
+    device address plus its offset; unaligned starts, non-contiguous views and arrays outside
+    every block map to None (host logic only: the block here is a registry entry, no device)."""
+    import numpy as np
+    base = np.zeros(256, np.float32)
+    p = base.ctypes.data
+    flib._blocks[p] = (base.nbytes, 0x7000_0000)
+    try:
+        assert flib.device_address(base).value == 0x7000_0000
+        assert flib.device_address(base[8:40]).value == 0x7000_0000 + 32
+        assert flib.device_address(base[1:9]) is None                 # 4-B aligned start
+        assert flib.device_address(base[1:9], align=4).value == 0x7000_0000 + 4
+        assert flib.device_address(base.reshape(16, 16)[:, :4]) is None  # not C-contiguous
+        assert flib.device_address(base.copy()) is None                # another allocation
+        assert flib.device_address([1.0, 2.0]) is None
+    finally:
+        flib._blocks.pop(p, None)
+    assert flib.device_address(base) is None
