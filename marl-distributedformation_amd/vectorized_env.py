@@ -171,7 +171,8 @@ class FormationEnv(_BASE):
         return _lib.current_stream(self.device)
 
     def release(self) -> None:
-        """Free this env's device state, its staging buffers and its host mirrors now.
+        """Free this env's device state and staging buffers now, and drop its host arrays (their
+        block goes back to the pool once no returned array views it).
 
         Idempotent.  Afterwards every device call raises.  The reference has no such path: its
         ``close()`` raises NotImplementedError (vectorized_env.py:87-88), which is kept, so this
