@@ -715,6 +715,12 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         e1.synchronize()
         return e0.elapsed_time(e1)
 
+    # one full collection now, then freeze what survives: the collection right before the timed
+    # region then only walks objects made since, instead of idling the GPU for a full
+    # generation-2 pass over every torch object (~40 ms) just before the first timed launch
+    if not args.no_gc_freeze:
+        gc.collect()
+        gc.freeze()
     pw_ms += prewarm_region()      # first use of everything (slow)
     last = prewarm_region()        # calibration: one warm region
     pw_ms += last
@@ -743,7 +749,10 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     if trace is not None:
         trace.clear()
     # no cyclic-GC pass inside the window (as timeit does): a generation-2 collection over the
-    # torch objects alive here takes far longer than the 20-step window
+    # torch objects alive here takes far longer than the 20-step window.  The objects made before
+    # the pre-warm are frozen, so this collection is short: a full one here idled the GPU ~40 ms
+    # right before the first timed launch, and the window then ran ~6 % slower (first launches
+    # slower, fixed overhead 60 vs 27 us; profiles/ab/r5_gc_freeze_ab.txt)
     gc.collect()
     gc.disable()
     t0 = time.perf_counter()
@@ -752,6 +761,8 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    if not args.no_gc_freeze:
+        gc.unfreeze()
     stamp("synchronized")
     # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
     # the slowest rank, and a barrier inside would add a collective's latency to every rank
@@ -878,6 +889,8 @@ def main():
                          "--warmup steps; independent of --warmup, reported as warmup_ms")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gc-freeze", action="store_true",
+                    help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--trace-host", action="store_true",
                     help="diagnostic: host timestamps (us after t0) of the timed region's calls")
