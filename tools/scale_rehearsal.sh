@@ -10,7 +10,7 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 export PYTHONUNBUFFERED=1
 for F in ${SIZES:-131072 262144 524288 1048576}; do
-  for rep in 1 2 3; do
+  for rep in $(seq 1 ${REPS:-3}); do
     timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 --formations $F --no-policy \
       --no-configs --no-cpu-baseline > "$O/shard_${F}_$rep.json" 2> "$O/shard_${F}_$rep.err" || exit $?
   done
