@@ -540,6 +540,75 @@ def hbm_ceiling(acts, obs, rew, done, A: int, T: int, D: int, stream, reps: int 
                       "faster of plain and non-temporal stores"}
 
 
+GATE_PREFIX = 64  # launches issued behind the launch gate before it is released (bench window)
+
+
+class _Gate:
+    """bench's launch gate: fenv_stream_gate on the launch stream over a word of device-mapped
+    host memory (include/fenv.h).  arm() enqueues the gate wave (a new release value each time),
+    release() stores the value from the host -- one plain memory write, no HIP call -- and
+    status() reads what the wave recorded.  probe() measures the release latency: the host stores
+    the value into an armed gate and spins until it sees the wave's status word, so one sample is
+    host store -> the wave's poll sees it -> its status store -> the host's read sees that."""
+
+    TIMEOUT_US = 5_000_000  # the wave exits after 5 s whatever the host does
+
+    def __init__(self, flib, L, dev, stream):
+        import ctypes
+        import numpy as np
+        self.L, self.flib = L, flib
+        self.blk = flib.HostBlock(dev, [("flag", np.uint32, (16,)), ("status", np.uint32, (16,))])
+        self.blk.flag[:] = 0
+        self.stream = ctypes.c_void_p(stream.cuda_stream)
+        self.value = 0
+        self.arm()      # first use (module load of the kernel) outside any window
+        self.release()
+        stream.synchronize()
+
+    def arm(self):
+        self.value = (self.value + 1) & 0xFFFFFFFF or 1
+        self.blk.status[:2] = 0
+        rc = self.L.fenv_stream_gate(self.blk.dev("flag"), self.value, self.TIMEOUT_US,
+                                     self.blk.dev("status"), self.stream)
+        if rc:
+            self.flib.check(rc, "fenv_stream_gate")
+
+    def release(self):
+        self.blk.flag[0] = self.value
+
+    def status(self) -> dict:
+        return {"released": int(self.blk.status[0]), "polls": int(self.blk.status[1])}
+
+    def probe(self, reps: int = 21) -> dict:
+        us = []
+        for _ in range(reps):
+            self.arm()
+            t = time.perf_counter()
+            while time.perf_counter() - t < 300e-6:  # the wave is polling by now
+                pass
+            t = time.perf_counter()
+            self.release()
+            while self.blk.status[0] == 0 and time.perf_counter() - t < 1.0:
+                pass
+            us.append((time.perf_counter() - t) * 1e6)
+        import torch
+        torch.cuda.synchronize()
+        us.sort()
+        return {"roundtrip_us_median": us[len(us) // 2], "roundtrip_us_max": us[-1],
+                "reps": reps,
+                "what": "host flag store -> gate wave sees it -> its status store reaches host "
+                        "memory -> the spinning host sees it (two bus crossings)"}
+
+
+def window_summary(w: dict, total_agents: int, steps: int) -> dict:
+    """The JSON fields of one timed window (max over ranks)."""
+    return {"value": total_agents * steps / w["elapsed_max"],
+            "kernel_value": total_agents * steps / (w["kern_ms_max"] * 1e-3),
+            "ms_per_step": w["elapsed_max"] * 1e3 / steps,
+            "fixed_overhead_ms": w["elapsed_max"] * 1e3 - w["kern_ms_max"],
+            "kernel_ms_timed": w["kern_ms_max"], "host_issue_ms": w["host_issue_ms"]}
+
+
 def launch_plan(steps: int, T: int) -> list[int]:
     """Launch lengths covering exactly `steps` env steps in fused chunks of <= T steps."""
     full, rem = divmod(int(steps), int(T))
@@ -671,7 +740,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         if trace is not None:
             trace.append((what, time.perf_counter()))
 
-    def region(plan, stat_every, evs=None):
+    def region(plan, stat_every, evs=None, release_after=None, release=None):
         """The timed region's work: the launches of `plan`, stats on the first launch of every
         `stat_every` (a stats launch's reduction is issued after the next launch, so it runs
         on the side stream under that launch), then the wait for the last stats (side stream /
@@ -679,7 +748,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         end right after the last.  No timing event goes between launches: the command processor
         idles the GPU ~12 us at each one (it completes the kernel and writes back the caches
         before it takes the timestamp; rocprofv3 kernel trace, profiles/r5_region_trace.txt),
-        where a launch after a plain kernel or a timing-free event starts at once."""
+        where a launch after a plain kernel or a timing-free event starts at once.
+        `release` (gated window) is called once launch `release_after` and the reductions issued
+        after it are queued, or at the end when that is the last launch."""
         n = len(plan)
         for k, L in enumerate(plan):
             launch(k, L, stat=not args.no_stats and k % stat_every == 0,
@@ -689,8 +760,12 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 evs[1].record(main_s)
             flush(before=k)
             stamp(f"stats before {k}")
+            if release is not None and k == release_after and k < n - 1:
+                release()
         flush(last=bool(pending) and pending[-1][0] == n - 1)
         stamp("last stats")
+        if release is not None and release_after >= n - 1:
+            release()
         # The last stats' buffer; nothing on the device consumes it, so no stream waits for the
         # side stream here: the caller's device-wide synchronize (every stream, RCCL's included)
         # completes it before the host reads it.
@@ -735,47 +810,102 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     # first timed launch
     plan = launch_plan(args.steps, T)
     stat_every = max(1, min(args.stats_every, len(plan)))
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    for e in evs:
-        e.record(main_s)
-    for L in launch_plan(args.warmup, T):
-        launch(-1, L)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    freed[0] = freed[1] = None  # the synchronize completed every reduction (no wait packets)
+    # The launch gate (include/fenv.h fenv_stream_gate): a one-wave kernel at the head of the main
+    # stream polls a word of device-mapped host memory; the window's launches, stats reductions
+    # and all-reduces are issued behind it, then the host takes t0 and stores the word.  Host
+    # issue -- and the random 80-250 us stalls inside post-synchronize HIP calls, which 2 of 7
+    # processes showed at the 8/4/2-way shard sizes (profiles/r5_shard_sweep_gcfreeze.txt) --
+    # leaves the window; every launch's device execution and the closing synchronize stay in it.
+    # Plans longer than GATE_PREFIX launches release the gate after the first GATE_PREFIX (the
+    # rest is issued while the device runs those: bounded queue depth).  MT19937 mode is host-issued:
+    # its refills can wait on the device for a consumed staging slot, which a held stream never
+    # frees.
+    gated = args.issue == "gated" and args.reset_mode == "philox"
+    gate = _Gate(flib, L_abi, dev, main_s) if gated else None
 
-    if trace is not None:
-        trace.clear()
-    # no cyclic-GC pass inside the window (as timeit does): a generation-2 collection over the
-    # torch objects alive here takes far longer than the 20-step window.  The objects made before
-    # the pre-warm are frozen, so this collection is short: a full one here idled the GPU ~40 ms
-    # right before the first timed launch, and the window then ran ~6 % slower (first launches
-    # slower, fixed overhead 60 vs 27 us; profiles/ab/r5_gc_freeze_ab.txt)
-    gc.collect()
-    gc.disable()
-    t0 = time.perf_counter()
-    tot = region(plan, stat_every, evs)
-    t_issued = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
+    def window(use_gate: bool):
+        """--warmup steps, a synchronize (+ barrier), then one timed window of `plan`."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for e in evs:
+            e.record(main_s)
+        for L in launch_plan(args.warmup, T):
+            launch(-1, L)
+        torch.cuda.synchronize()
+        if pdist.active():
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        freed[0] = freed[1] = None  # the synchronize completed every reduction (no wait packets)
+        if trace is not None:
+            trace.clear()
+        # no cyclic-GC pass inside the window (as timeit does): a generation-2 collection over the
+        # torch objects alive here takes far longer than the 20-step window.  The objects made
+        # before the pre-warm are frozen, so this collection is short: a full one here idled the
+        # GPU ~40 ms right before the first timed launch, and the window then ran ~6 % slower
+        # (first launches slower, fixed overhead 60 vs 27 us; profiles/ab/r5_gc_freeze_ab.txt)
+        gc.collect()
+        gc.disable()
+        w = {}
+        if use_gate:
+            t_arm = time.perf_counter()
+            gate.arm()
+            rel = min(len(plan), GATE_PREFIX) - 1
+            t0 = None
+
+            def release():
+                nonlocal t0
+                w["prefix_issue_ms"] = (time.perf_counter() - t_arm) * 1e3
+                t0 = time.perf_counter()
+                gate.release()
+                stamp("gate released")
+
+            tot = region(plan, stat_every, evs, release_after=rel, release=release)
+        else:
+            t0 = time.perf_counter()
+            tot = region(plan, stat_every, evs)
+        t_issued = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        gc.enable()
+        stamp("synchronized")
+        w.update(elapsed=elapsed, host_issue_ms=t_issued * 1e3, tot=tot,
+                 kern_ms=evs[0].elapsed_time(evs[1]), t0=t0,
+                 trace=None if trace is None else [(k, round((t - t0) * 1e6, 2))
+                                                   for k, t in trace])
+        if use_gate:
+            w["gate"] = gate.status()
+            w["gate"]["prefix_launches"] = min(len(plan), GATE_PREFIX)
+            if w["gate"]["released"] != 1:  # the gate timed out: the window is not a measurement
+                raise RuntimeError(f"launch gate did not release: {w['gate']}")
+        # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
+        # the slowest rank, and a barrier inside would add a collective's latency to every rank
+        if pdist.active():
+            torch.distributed.barrier()
+        return w
+
+    # the host-issued window first (rounds 1-5's measurement), then the gated one (the headline)
+    w_host = window(False)
+    w_gate = window(True) if gated else None
     if not args.no_gc_freeze:
         gc.unfreeze()
-    stamp("synchronized")
-    # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
-    # the slowest rank, and a barrier inside would add a collective's latency to every rank
-    if world > 1:
-        torch.distributed.barrier()
-    kern_total_ms = evs[0].elapsed_time(evs[1])
+    head = w_gate or w_host
+    gate_probe = gate.probe() if gated else None  # after both windows
     ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
     # the same byte mix over the first 4 planes only: its 0.17 GB of actions stay in the 256 MB
     # Infinity Cache from one k_mix launch to the next, so this is NOT an HBM ceiling -- it shows
     # what the launch's re-read actions cost it (DESIGN.md §4.1, profiles/r5_footprint_ubench.txt)
     ceiling_small = hbm_ceiling(acts[0], obs, rew, done, A, min(T, 4), D, main_s)
-    elapsed = pdist.max_over_ranks(elapsed, dev)
-    kern_total_ms = pdist.max_over_ranks(kern_total_ms, dev)
+    # per-rank timings of both windows (one all-gather), then the max over ranks
+    wins = [w for w in (w_host, w_gate) if w is not None]
+    mine = [x for w in wins for x in (w["elapsed"] * 1e3, w["kern_ms"], w["host_issue_ms"])]
+    per = pdist.gather_floats(mine, dev)
+    per_rank = []
+    for i, w in enumerate(wins):
+        cols = [[r[3 * i + j] for r in per] for j in range(3)]
+        per_rank.append({"elapsed_ms": cols[0], "kernel_ms": cols[1], "host_issue_ms": cols[2]})
+        w["elapsed_max"] = max(cols[0]) * 1e-3
+        w["kern_ms_max"] = max(cols[1])
+    elapsed, kern_total_ms, tot = head["elapsed_max"], head["kern_ms_max"], head["tot"]
+    t_issued = head["host_issue_ms"] * 1e-3
 
     steps = sum(plan)
     kern_avg_ms = kern_total_ms * T / steps  # per T-step launch (equal to the mean when uniform)
@@ -811,8 +941,13 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "host_issue_ms": t_issued * 1e3,
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
-            **({"host_trace_us": [(w, round((t - t0) * 1e6, 2)) for w, t in trace]}
-               if trace is not None else {}),
+            "issue": "gated" if head is w_gate else "host",
+            **({"gate": {**head["gate"], "release_probe": gate_probe,
+                         "prefix_issue_ms": head["prefix_issue_ms"]}} if head is w_gate else {}),
+            "host_issued": window_summary(w_host, total_agents, steps),
+            **({"per_rank": {"host": per_rank[0], **({"gated": per_rank[1]} if gated else {})}}
+               if pdist.active() else {}),
+            **({"host_trace_us": head["trace"]} if trace is not None else {}),
             "config": {"workload": workload, "formations": total_formations,
                        "agents_per_formation": N, "obs_dim": D, "rollout_chunk": T,
                        "formations_per_gpu": F, "reset_mode": args.reset_mode,
@@ -889,6 +1024,10 @@ def main():
                          "--warmup steps; independent of --warmup, reported as warmup_ms")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--issue", default="gated", choices=["gated", "host"],
+                    help="gated (philox): the window's launches are queued behind a launch gate "
+                         "released at t0, so host issue is outside it; the host-issued window is "
+                         "measured too and nested as host_issued.  host: host-issued only")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
@@ -928,6 +1067,11 @@ def main():
     # weak line (1,048,576 formations on every GPU) rides along as a nested measurement
     total = args.formations if scaling == "strong" else args.formations * world
     out, env = run_config3(args, pkg, rank, world, dev, total, scaling)
+    if rank == 0:
+        # the collectives of the line (stats all-reduce, barriers, max over ranks): "none" when no
+        # process group is up (the driver's N = 1 run); FENV_DIST_FORCE=1 runs them at world 1
+        out["dist"] = {"backend": torch.distributed.get_backend() if pdist.active() else "none",
+                       "world": world}
     env.release()
     del env
     if world > 1 and not args.no_weak_line:
@@ -938,8 +1082,8 @@ def main():
         del env2
         if rank == 0:
             keep = ("value", "kernel_value", "fixed_overhead_ms", "ms_per_step", "scaling",
-                    "config", "roofline", "steps")
-            out[f"{other}_scaling_line"] = {k: o2[k] for k in keep}
+                    "config", "roofline", "steps", "issue", "gate", "host_issued", "per_rank")
+            out[f"{other}_scaling_line"] = {k: o2[k] for k in keep if k in o2}
     if rank == 0:
         if world == 1 and not args.no_policy:
             out["policy_rollout"] = secondary(policy_rollout_bench, pkg.__name__, dev, 65536, 10,
@@ -963,7 +1107,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, D, args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pdist.active():
         torch.distributed.destroy_process_group()
 
 

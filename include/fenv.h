@@ -37,8 +37,9 @@ extern "C" {
  *        ppo_update_ws, ppo_grad, ppo_apply, fenv_test_ppo_inject
  *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes, fenv_debug_staging (no
  *        signature changed)
- *   4  + fenv_host_alloc, fenv_host_free (no signature changed) */
-#define FENV_ABI_VERSION 4
+ *   4  + fenv_host_alloc, fenv_host_free (no signature changed)
+ *   5  + fenv_stream_gate (no signature changed) */
+#define FENV_ABI_VERSION 5
 int fenv_abi_version(void);
 
 typedef struct fenv fenv_t;
@@ -170,6 +171,19 @@ const char *fenv_rollout_kernel(const fenv_t *env, int32_t T);
 /* Deterministic fixed-order reduction of `count` partial records into out[2] (double, device):
  * {sum of rewards, sum of agent-dones}. */
 int fenv_reduce_partials(const float *partial, int64_t count, double *out, void *stream);
+
+/* Launch gate (no reference counterpart: the reference steps one Python loop, vectorized_env.py
+ * :71-79).  Enqueues one wavefront on `stream` that holds every later launch on the stream until the
+ * 32-bit word at `flag` equals `value`, or until timeout_us (0 < timeout_us <= 60 s) of the device's
+ * constant-rate clock have passed -- the wave always exits, so a host that never stores the value
+ * costs the stream timeout_us, never a hang.  `flag` is a device address, normally inside a
+ * fenv_host_alloc block (the host stores the value with a plain write; the kernel polls it with
+ * system-scope loads over the bus).  status (device address, may be NULL; 8 bytes) receives
+ * status[0] = 1 (released by the flag) or 2 (timed out) and status[1] = the number of polls.
+ * Use: enqueue a batch of launches behind the gate, then release it, so the host's issue time of
+ * the batch is off the device's critical path (bench.py's timed region). */
+int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, uint32_t *status,
+                     void *stream);
 
 /* Per-formation statistics the reference logs to wandb (rew [A] may be NULL -> 0), out [F][8] f32:
  *   0 avg_dist_to_goal, 1 ave_dist_to_neighbor, 2 std_dist_to_neighbor (unbiased, NaN when

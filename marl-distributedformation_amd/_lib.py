@@ -45,6 +45,7 @@ SIGNATURES = {
     "fenv_partial_count": (_I64, [_P]),
     "fenv_rollout_kernel": (ctypes.c_char_p, [_P, _I32]),
     "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
+    "fenv_stream_gate": (_I32, [_P, _U32, _I64, _P, _P]),
     "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),
     "fenv_get_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
     "fenv_get_state_range": (_I32, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P]),
@@ -183,8 +184,8 @@ def require_device(device=None) -> torch.device:
     return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
 
 
-# live HostBlocks: host address -> (bytes, device address), for device_address()
-_blocks: dict[int, tuple[int, int]] = {}
+# live HostBlocks: host address -> (bytes, device address, device index), for device_address()
+_blocks: dict[int, tuple[int, int, int]] = {}
 
 
 def _host_free(device: int, host: int) -> None:
@@ -193,17 +194,21 @@ def _host_free(device: int, host: int) -> None:
         _lib.fenv_host_free(device, ctypes.c_void_p(host))
 
 
-def device_address(a: np.ndarray, align: int = 16) -> ctypes.c_void_p | None:
+def device_address(a: np.ndarray, device=None, align: int = 16) -> ctypes.c_void_p | None:
     """The device address of a C-contiguous numpy array that lies inside a live HostBlock (e.g.
     an observation array a FormationEnv's numpy face returned), so a kernel can read it in place;
-    None for any other array, or one not aligned to ``align`` bytes."""
+    None for any other array, one not aligned to ``align`` bytes, or (``device`` given) one whose
+    block was mapped for another device: a block's device address is only valid on its own."""
     if not isinstance(a, np.ndarray) or not a.flags.c_contiguous:
         return None
     p = a.ctypes.data
     if p % align:
         return None
-    for base, (n, dev) in _blocks.copy().items():  # a finalizer may drop a block meanwhile
+    want = None if device is None else torch.device(device).index
+    for base, (n, dev, di) in _blocks.copy().items():  # a finalizer may drop a block meanwhile
         if base <= p and p + a.nbytes <= base + n:
+            if want is not None and want != di:
+                return None
             return ctypes.c_void_p(dev + (p - base))
     return None
 
@@ -227,7 +232,7 @@ class HostBlock:
         raw = (ctypes.c_uint8 * max(total, 256)).from_address(h.value)
         # freed with the last view: the arrays below hold `raw` through their base chain
         weakref.finalize(raw, _host_free, device.index, h.value)
-        _blocks[h.value] = (max(total, 256), d.value)
+        _blocks[h.value] = (max(total, 256), d.value, device.index)
         base = np.ctypeslib.as_array(raw)
         self._dev = {}
         for name, dt, shape in fields:

@@ -22,8 +22,11 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return first, count
 
 
-def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
-    """Initialise torch.distributed from torchrun's env vars when WORLD_SIZE > 1.
+def init_from_env(backend: str | None = None, force: bool | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun's env vars when WORLD_SIZE > 1, or at any world
+    size when ``force`` (default: env ``FENV_DIST_FORCE=1``) -- a world-1 process group runs every
+    collective of the N > 1 path for real (the one-GPU box's way to execute RCCL: it refuses two
+    ranks on one GPU).
 
     Returns (rank, world_size, local_rank).  backend defaults to "nccl" (RCCL on ROCm) when a
     GPU is visible, else "gloo"."""
@@ -34,7 +37,9 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     backend = backend or os.environ.get("FENV_DIST_BACKEND") or None
     if torch.cuda.is_available() and torch.cuda.device_count() > 0:
         local = local % torch.cuda.device_count()
-    if world > 1 and not dist.is_initialized():
+    if force is None:
+        force = os.environ.get("FENV_DIST_FORCE", "") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if torch.cuda.is_available():
@@ -48,16 +53,23 @@ class StatsReducer:
 
     ``submit(v)`` starts an async all-reduce of ``v`` IN PLACE on a side stream, after the
     current stream's work that produced v (or after the event ``after``); the caller alternates
-    two buffers and must not overwrite a buffer until the submission two calls later (``submit``
-    then waits for the collective that used the same slot).  ``result()`` makes the current
-    stream (or ``stream``) wait for the last submission and returns its buffer.  With world
-    size 1 there is nothing to reduce and ``v`` is returned as is.
+    two buffers.  Before rewriting the buffer of a slot, call ``reserve()``: on the GPU it makes the
+    writing stream wait (device-side) for the all-reduce that last used the slot, on the CPU the
+    host waits for it.  ``result()`` makes the current stream (or ``stream``) wait for the last
+    submission and returns its buffer.  Without an initialised process group there is nothing to
+    reduce and ``v`` is returned as is; with one (any world size, world 1 included) every
+    submission is a real collective.
 
     Every cross-stream dependency goes through events created and recorded once in the
     constructor: torch's ``Stream.wait_stream`` creates and records a fresh event per call, and
     a torch event is created lazily at its first record -- host work that would otherwise sit
     inside a caller's timed region (bench.py).  ``stream`` lets the caller hand in the side
-    stream it already reduces on, so the collective adds no stream hop."""
+    stream it already reduces on, so the collective adds no stream hop.
+
+    Backends: on NCCL (RCCL) ``all_reduce(async_op=True).wait()`` only orders the side stream
+    after the collective, so ``submit`` returns at once.  On gloo with CUDA tensors the same
+    ``wait()`` blocks the host until the collective is done, so ``submit`` is synchronous there:
+    a gloo rehearsal (tools/scale_rehearsal.sh) does not measure the overlapped stats path."""
 
     def __init__(self, n: int, device, stream=None):
         self.device = torch.device(device)
@@ -65,7 +77,8 @@ class StatsReducer:
         self.bufs = [None, None]
         self.k = 0
         self.cuda = self.device.type == "cuda"
-        self.dist = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.dist = active()
+        self.used = [False, False]
         self.side = None
         if self.cuda:
             self.side = stream if stream is not None else torch.cuda.Stream(self.device)
@@ -74,10 +87,15 @@ class StatsReducer:
             for e in [self.dep] + self.done:
                 e.record(self.side)
 
-    def reserve(self) -> None:
-        """Make the current stream wait until the next slot's previous all-reduce finished
-        (call before overwriting the buffer you are about to submit)."""
+    def reserve(self, stream=None) -> None:
+        """Order a rewrite of the next slot's buffer after the all-reduce that last used the slot
+        (call before overwriting the buffer you are about to submit): on the GPU the current
+        stream (or ``stream``) waits for that submission's event, on the CPU the host waits."""
         s = self.k % 2
+        if self.cuda:
+            if self.used[s]:
+                (stream or torch.cuda.current_stream(self.device)).wait_event(self.done[s])
+            return
         if self.work[s] is not None:
             self.work[s].wait()
             self.work[s] = None
@@ -100,6 +118,7 @@ class StatsReducer:
                     # stream-ordered: wait() only makes the side stream wait for the collective
                     dist.all_reduce(v, async_op=True).wait()
                 self.done[s].record(st)
+            self.used[s] = True
         else:
             self.reserve()
             if self.dist:
@@ -120,12 +139,30 @@ class StatsReducer:
         return self.bufs[s]
 
 
+def active() -> bool:
+    """True when a process group is initialised: the collectives run (any world size)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def max_over_ranks(x: float, device=None) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    """Max of ``x`` over the ranks (one all-reduce; ``x`` itself without a process group)."""
+    if not active():
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_floats(xs, device=None) -> list[list[float]]:
+    """All-gather of a short list of floats from every rank -> one list per rank, in rank order
+    (one collective; [xs] without a process group)."""
+    xs = [float(x) for x in xs]
+    if not active():
+        return [xs]
+    t = torch.tensor(xs, dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
 
 
 def world_rank() -> tuple[int, int]:

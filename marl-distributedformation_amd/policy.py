@@ -148,6 +148,8 @@ class MlpPolicy:
         if offset is None:
             offset = self._offset
             self._offset += 1
+        if B == 0:  # nothing to launch (an empty tensor's data pointer is NULL)
+            return out
         s = self.sample_seed if seed is None else seed
         _lib.check(_lib.lib().policy_forward(
             _lib.ptr(self.flat), self.obs_dim, _lib.ptr(obs), B, int(row0), _lib.ptr(out.get("mu")),
@@ -164,7 +166,8 @@ class MlpPolicy:
         The kernel reads the observations and writes the actions in device-mapped host memory
         (``_lib.HostBlock``): observations a FormationEnv's numpy face returned are read in place,
         others are first copied into the policy's block; the actions come back as a new array.
-        Same bits and the same noise offset advance as ``forward(...)["clipped"]``."""
+        Same bits and the same noise offset advance as ``forward(...)["clipped"]`` (an empty batch
+        included: it advances the offset and launches nothing)."""
         if isinstance(observation, torch.Tensor) and observation.is_cuda:
             return self.forward(observation, deterministic=deterministic)["clipped"].cpu().numpy(), None
         obs = np.asarray(observation, np.float32)
@@ -172,13 +175,14 @@ class MlpPolicy:
             raise ValueError(f"obs must be [B, {self.obs_dim}]")
         B = obs.shape[0]
         if B == 0:
+            self._offset += 1  # as forward() on an empty batch
             return np.zeros((0, 2), np.float32), None
         host = self._host.get(B)
         if host is None:
             host = _lib.HostBlock(self.device, [("obs", np.float32, (B, self.obs_dim)),
                                                 ("clipped", np.float32, (B, 2))])
             self._host = {B: host}  # one batch size cached (playback and SB3 loops keep theirs)
-        d_obs = _lib.device_address(obs)
+        d_obs = _lib.device_address(obs, self.device)
         if d_obs is None:
             np.copyto(host.obs, obs)
             d_obs = host.dev("obs")

@@ -263,13 +263,16 @@ def test_destroy_of_unknown_handle_is_refused(flib):
 def test_device_address_lookup(flib):
     """``_lib.device_address``: an array inside a registered host block maps to the block's
     device address plus its offset; unaligned starts, non-contiguous views and arrays outside
-    every block map to None (host logic only: the block here is a registry entry, no device)."""
+    every block map to None, and so does a block mapped for another device than the one asked
+    for (host logic only: the block here is a registry entry, no device)."""
     import numpy as np
     base = np.zeros(256, np.float32)
     p = base.ctypes.data
-    flib._blocks[p] = (base.nbytes, 0x7000_0000)
+    flib._blocks[p] = (base.nbytes, 0x7000_0000, 1)
     try:
         assert flib.device_address(base).value == 0x7000_0000
+        assert flib.device_address(base, "cuda:1").value == 0x7000_0000
+        assert flib.device_address(base, "cuda:0") is None            # mapped for device 1
         assert flib.device_address(base[8:40]).value == 0x7000_0000 + 32
         assert flib.device_address(base[1:9]) is None                 # 4-B aligned start
         assert flib.device_address(base[1:9], align=4).value == 0x7000_0000 + 4
@@ -279,3 +282,15 @@ def test_device_address_lookup(flib):
     finally:
         flib._blocks.pop(p, None)
     assert flib.device_address(base) is None
+
+
+def test_stream_gate_argument_errors(flib):
+    """fenv_stream_gate validates its arguments before any HIP call: a NULL flag or a timeout
+    outside (0, 60 s] is FENV_EINVAL (no device needed)."""
+    import ctypes
+    L = flib.lib()
+    flag = ctypes.c_void_p(0x1000)
+    assert L.fenv_stream_gate(None, 1, 1000, None, None) == -1
+    assert b"fenv_stream_gate" in L.fenv_last_error()
+    assert L.fenv_stream_gate(flag, 1, 0, None, None) == -1
+    assert L.fenv_stream_gate(flag, 1, 60_000_001, None, None) == -1

@@ -19,6 +19,46 @@ def _free_port():
     return p
 
 
+def _world1_worker(port, root, q):
+    """FENV_DIST_FORCE=1 at WORLD_SIZE 1: a real process group, so every collective of the N > 1
+    path runs (the StatsReducer all-reduce, max_over_ranks, gather_floats, the barrier)."""
+    import sys
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0", FENV_DIST_FORCE="1")
+    import pkgload
+    from importlib import import_module
+    d = import_module(pkgload.load().__name__ + ".distributed")
+    r, w, _ = d.init_from_env(backend="gloo")
+    red = d.StatsReducer(2, "cpu")
+    bufs = [torch.zeros(2, dtype=torch.float64) for _ in range(2)]
+    for k in range(3):
+        red.reserve()
+        bufs[k % 2].copy_(torch.tensor([float(k), 2.0], dtype=torch.float64))
+        red.submit(bufs[k % 2])
+    res = red.result().tolist()
+    dist.barrier()
+    q.put((r, w, d.active(), red.dist, res, d.max_over_ranks(4.5), d.gather_floats([1.0, 2.0]),
+           dist.get_backend()))
+    dist.destroy_process_group()
+
+
+def test_forced_world1_process_group_runs_collectives():
+    """The N > 1 code path at world size 1 (how the one-GPU box executes RCCL once, tests/
+    test_gpu_rccl.py): FENV_DIST_FORCE=1 makes init_from_env start a process group, and the
+    stats reducer, max_over_ranks and gather_floats then go through real collectives."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_worker, args=(_free_port(), root, q))
+    p.start()
+    r, w, active, red_dist, res, mx, per, backend = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert (r, w, active, red_dist, backend) == (0, 1, True, True, "gloo")
+    assert res == [2.0, 2.0] and mx == 4.5 and per == [[1.0, 2.0]]
+
+
 def test_shard_range_partitions(pkg):
     from importlib import import_module
     d = import_module(pkg.__name__ + ".distributed")
@@ -72,6 +112,7 @@ def _worker(rank, world, port, root, q):
         red.submit(bufs[k % 2])
     out = red.result().clone()
     mx = d.max_over_ranks(float(rank) * 3.0)
+    per = d.gather_floats([rank, rank * 2.5, -1.0])  # bench's per-rank timings
     # PPO's collectives: rank 0's parameters replicated once; per update ONE all-gather of the
     # [T, A_r, D+5] samples of uneven shards (11 formations x 5 agents: 30 + 25 rows)
     params = torch.full((9669,), float(rank + 1))
@@ -88,7 +129,7 @@ def _worker(rank, world, port, root, q):
     got = [None] * world
     dist.all_gather_object(got, (gathered.numpy().tobytes(), perms.numpy().tobytes()))
     if rank == 0:
-        q.put((parts, out.tolist(), mx, float(params.sum()), counts, got))
+        q.put((parts, out.tolist(), mx, float(params.sum()), counts, got, per))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -101,7 +142,7 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q)) for r in range(2)]
     for p in procs:
         p.start()
-    parts, out, mx, psum, counts, got = q.get(timeout=120)
+    parts, out, mx, psum, counts, got, per = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -118,6 +159,7 @@ def test_gloo_world2_sharded_draws_and_stats(flib):
     assert np.array_equal(np.concatenate([np.array(p[2], np.float32) for p in parts]), gx)
     assert out == [float(0 + 4) + float(1 + 4), 2.0]
     assert mx == 3.0
+    assert per == [[0.0, 0.0, -1.0], [1.0, 2.5, -1.0]]  # one list per rank, in rank order
     assert psum == 9669.0                        # rank 0's ones everywhere
     assert counts == [30, 25]                    # uneven shards (6 + 5 formations)
     # both ranks gathered the same buffer, equal to the unsharded (world-1) one, and drew the

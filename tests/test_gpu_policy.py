@@ -190,4 +190,10 @@ def test_predict_zero_copy_matches_forward(pkg, pol_mod):
         assert np.array_equal(got, snap)
     with pytest.raises(ValueError):
         pol.predict(np.zeros((4, 6), np.float32))
+    # an empty batch advances the noise offset exactly as forward() does
+    off = pol._offset
+    got, _ = pol.predict(np.zeros((0, 8), np.float32))
+    assert got.shape == (0, 2) and pol._offset == off + 1
+    pol.forward(torch.zeros((0, 8), device=DEV))
+    assert pol._offset == off + 2
     env.release()

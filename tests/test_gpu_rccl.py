@@ -1,0 +1,62 @@
+"""GPU: RCCL executed once on the one-GPU box (RCCL refuses two ranks on one GPU, so the
+driver's 8-GPU run would otherwise be its first execution).  bench.py's N > 1 region --
+the stats reductions' side-stream all-reduce, max_over_ranks, the per-rank all-gather and the
+barriers -- runs in a world-1 process group over backend "nccl" (FENV_DIST_FORCE=1), and its
+episode statistics equal, bit for bit, those of the same command with no process group."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the 8-way shard size of config 3; --prewarm-ms 0: a fixed pre-warm (2 regions), so both runs
+# step the env through the same launches
+ARGS = ["--gpus", "1", "--steps", "20", "--warmup", "5", "--formations", "131072",
+        "--prewarm-ms", "0", "--no-policy", "--no-configs", "--no-cpu-baseline"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(env_extra):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FENV_DIST_FORCE", "FENV_DIST_BACKEND"):
+        env.pop(k, None)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + ARGS, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_region_over_rccl_world1():
+    plain = _bench({})
+    rccl = _bench({"FENV_DIST_FORCE": "1", "FENV_DIST_BACKEND": "nccl", "WORLD_SIZE": "1",
+                   "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                   "MASTER_PORT": str(_port())})
+    assert plain["dist"] == {"backend": "none", "world": 1}
+    assert rccl["dist"] == {"backend": "nccl", "world": 1}
+    for d in (plain, rccl):
+        assert d["issue"] == "gated" and d["gate"]["released"] == 1
+        assert d["value"] > 0 and d["host_issued"]["value"] > 0
+    # the per-rank timings came through the all-gather (one rank), and agree with the line
+    pr = rccl["per_rank"]
+    assert set(pr) == {"host", "gated"}
+    for w in pr.values():
+        assert all(len(v) == 1 for v in w.values())
+    assert abs(pr["gated"]["elapsed_ms"][0] - rccl["ms_per_step"] * rccl["steps"]) < 1e-6
+    assert "per_rank" not in plain
+    # the all-reduced stats equal the unreduced ones bit for bit (same seed, same launches)
+    assert rccl["episode_stats"] == plain["episode_stats"]
+    assert rccl["episode_stats"]["agent_dones_sampled_rollout"] >= 0

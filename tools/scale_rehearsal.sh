@@ -1,7 +1,8 @@
 #!/bin/bash
 # bench.py's timed region at the shard sizes of an 8/4/2/1-GPU strong-scaling run of config 3
 # (131072, 262144, 524288, 1048576 formations on one GPU, the driver's --steps 20 --warmup 5):
-# wall vs event-timed kernel time and the fixed overhead per size; then the bench's N > 1 path
+# the fixed overhead (wall - event-timed kernel span) of the gated window and of the host-issued
+# window nested in the same line, per size; then the bench's N > 1 path
 # with two ranks on the one GPU over gloo (its rate says nothing about scaling).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,11 +22,15 @@ rows = {}
 for f in sorted(glob.glob(sys.argv[1] + "/shard_*_*.json")):
     d = json.load(open(f))
     F = d["config"]["formations"]
-    rows.setdefault(F, []).append((d["ms_per_step"] * d["steps"], d["roofline"]["kernel_ms_timed"],
-                                   d["fixed_overhead_ms"] * 1e3, d["value"], d["kernel_value"]))
+    h = d.get("host_issued", d)
+    rows.setdefault(F, []).append((d.get("issue", "host"), d["fixed_overhead_ms"] * 1e3,
+                                   h["fixed_overhead_ms"] * 1e3, d["value"], h["value"],
+                                   d["kernel_value"]))
 for F, v in sorted(rows.items()):
-    print(F, " | ".join(f"wall {a:.4f} ms kern {b:.4f} ms fixed {c:.1f} us value {e:.3e} kv {g:.3e}"
-                        for a, b, c, e, g in v))
+    print(F, "fixed us (%s):" % v[0][0], " ".join("%.1f" % r[1] for r in v),
+          "| host-issued fixed us:", " ".join("%.1f" % r[2] for r in v))
+    print(F, "value:", " ".join("%.3e" % r[3] for r in v), "| host-issued value:",
+          " ".join("%.3e" % r[4] for r in v), "| kernel_value:", " ".join("%.3e" % r[5] for r in v))
 PY
 if [ -z "${SKIP_GLOO:-}" ]; then
   FENV_DIST_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
