@@ -13,12 +13,14 @@ this module writes and reads the SB3 2.x ``save_to_zip_file`` layout itself:
     system_info.txt             text
 
 Loading reads ``policy.pth`` with ``torch.load(weights_only=True)`` only (no pickle
-execution), so zips written by real SB3 load here too.  Zips written here carry the same entry
+execution), so zips written by real SB3 should load here too (unverified: no SB3-written zip
+exists here).  Zips written here carry the same entry
 names and tensors.  SB3's ``data`` entries for ``policy_class``, ``observation_space`` and
 ``action_space`` are cloudpickled SB3 / gymnasium objects; round 4 writes them as the pickles
 cloudpickle would (``sb3_pickle.py``: the policy class by reference, the reference's two
 ``Box`` spaces), so the reference's own playback, ``PPO.load(checkpoint_path)`` with no
-``custom_objects`` (visualize_policy.py:35), has what it needs.  The Adam state's param group
+``custom_objects`` (visualize_policy.py:35), should have what it needs (designed for, not run:
+SB3 is absent).  The Adam state's param group
 is written with SB3's optimizer settings (non-capturable Adam), so ``set_parameters`` loads it
 on any device.  Parity against SB3 itself: unpinned (SB3 and gymnasium absent).
 """

@@ -14,7 +14,10 @@ a console log every ``log_interval`` rollouts.
 Extra keys (all optional, hydra ``key=value`` syntax): ``num_steps`` (5000, the reference's
 constant), ``seed`` (env + policy seed), ``reset_mode`` (mt19937 | philox), ``batch_size`` /
 ``n_epochs`` (SB3 defaults 64 / 10), ``log_interval`` (4).  With several ranks the formations are
-sharded contiguously and the flat gradient is all-reduced once per optimizer step (RCCL).
+sharded contiguously.  The default update mode is "replicated" (ppo.py ``PPOConfig.update_mode``):
+one all-gather of every rank's rollout samples per update (RCCL), then the same update on every
+rank, with no gradient all-reduce; ``update_mode="sharded"`` instead all-reduces the flat gradient
+once per global minibatch.
 """
 from __future__ import annotations
 
