@@ -565,11 +565,14 @@ class _Gate:
         self.release()
         stream.synchronize()
 
-    def arm(self):
+    def arm(self, exit_event=None):
+        """Enqueue the gate wave; `exit_event` (a created torch.cuda.Event) is bound to its exit."""
+        import ctypes
         self.value = (self.value + 1) & 0xFFFFFFFF or 1
         self.blk.status[:2] = 0
+        ev = None if exit_event is None else ctypes.c_void_p(exit_event.cuda_event)
         rc = self.L.fenv_stream_gate(self.blk.dev("flag"), self.value, self.TIMEOUT_US,
-                                     self.blk.dev("status"), self.stream)
+                                     self.blk.dev("status"), ev, self.stream)
         if rc:
             self.flib.check(rc, "fenv_stream_gate")
 
@@ -740,7 +743,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         if trace is not None:
             trace.append((what, time.perf_counter()))
 
-    def region(plan, stat_every, evs=None, release_after=None, release=None):
+    def region(plan, stat_every, evs=None, release_after=None, release=None, bound=False):
         """The timed region's work: the launches of `plan`, stats on the first launch of every
         `stat_every` (a stats launch's reduction is issued after the next launch, so it runs
         on the side stream under that launch), then the wait for the last stats (side stream /
@@ -750,14 +753,21 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         before it takes the timestamp; rocprofv3 kernel trace, profiles/r5_region_trace.txt),
         where a launch after a plain kernel or a timing-free event starts at once.
         `release` (gated window) is called once launch `release_after` and the reductions issued
-        after it are queued, or at the end when that is the last launch."""
+        after it are queued, or at the end when that is the last launch.  `bound`: evs[0] is
+        already bound to the gate wave's exit, and evs[1] is bound to the start of an empty
+        mark kernel after the last launch (fenv_stream_mark) -- no marker packet in the window."""
         n = len(plan)
         for k, L in enumerate(plan):
             launch(k, L, stat=not args.no_stats and k % stat_every == 0,
-                   ev=evs[0] if (evs is not None and k == 0) else None)
+                   ev=evs[0] if (evs is not None and k == 0 and not bound) else None)
             stamp(f"launch {k}")
             if evs is not None and k == n - 1:
-                evs[1].record(main_s)
+                if bound:
+                    rc = L_abi.fenv_stream_mark(vp(evs[1].cuda_event), abi_stream)
+                    if rc:
+                        flib.check(rc, "fenv_stream_mark")
+                else:
+                    evs[1].record(main_s)
             flush(before=k)
             stamp(f"stats before {k}")
             if release is not None and k == release_after and k < n - 1:
@@ -817,11 +827,16 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     # processes showed at the 8/4/2-way shard sizes (profiles/r5_shard_sweep_gcfreeze.txt) --
     # leaves the window; every launch's device execution and the closing synchronize stay in it.
     # Plans longer than GATE_PREFIX launches release the gate after the first GATE_PREFIX (the
-    # rest is issued while the device runs those: bounded queue depth).  MT19937 mode is host-issued:
-    # its refills can wait on the device for a consumed staging slot, which a held stream never
-    # frees.
-    gated = args.issue == "gated" and args.reset_mode == "philox"
+    # rest is issued while the device runs those: bounded queue depth).  Host-issued instead:
+    # MT19937 mode (its refills can wait on the device for a consumed staging slot, which a held
+    # stream never frees) and a gloo process group (gloo's wait() on a CUDA tensor's all-reduce
+    # blocks the host until the tensor's producer -- held behind the gate -- has run).
+    gated = (args.issue == "gated" and args.reset_mode == "philox"
+             and (not pdist.active() or torch.distributed.get_backend() == "nccl"))
     gate = _Gate(flib, L_abi, dev, main_s) if gated else None
+    # gated window's timing events: bound to the gate wave's exit and to an empty kernel's start
+    # after the last launch (args.marks "bound"), or hipEventRecord markers ("events")
+    bound_marks = gated and args.marks == "bound"
 
     def window(use_gate: bool):
         """--warmup steps, a synchronize (+ barrier), then one timed window of `plan`."""
@@ -847,7 +862,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         w = {}
         if use_gate:
             t_arm = time.perf_counter()
-            gate.arm()
+            gate.arm(evs[0] if bound_marks else None)
             rel = min(len(plan), GATE_PREFIX) - 1
             t0 = None
 
@@ -855,10 +870,15 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 nonlocal t0
                 w["prefix_issue_ms"] = (time.perf_counter() - t_arm) * 1e3
                 t0 = time.perf_counter()
+                # host clocks of the store, to place it on a rocprofv3 kernel trace's time axis
+                # (tools/gate_latency.py: store -> gate wave exit -> first launch start)
+                w["release_clock_ns"] = {"boottime": time.clock_gettime_ns(time.CLOCK_BOOTTIME),
+                                         "monotonic": time.monotonic_ns()}
                 gate.release()
                 stamp("gate released")
 
-            tot = region(plan, stat_every, evs, release_after=rel, release=release)
+            tot = region(plan, stat_every, evs, release_after=rel, release=release,
+                         bound=bound_marks)
         else:
             t0 = time.perf_counter()
             tot = region(plan, stat_every, evs)
@@ -942,8 +962,11 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
             "issue": "gated" if head is w_gate else "host",
+            "marks": "bound" if head is w_gate and bound_marks else "events",
             **({"gate": {**head["gate"], "release_probe": gate_probe,
-                         "prefix_issue_ms": head["prefix_issue_ms"]}} if head is w_gate else {}),
+                         "prefix_issue_ms": head["prefix_issue_ms"],
+                         "release_clock_ns": head["release_clock_ns"]}}
+               if head is w_gate else {}),
             "host_issued": window_summary(w_host, total_agents, steps),
             **({"per_rank": {"host": per_rank[0], **({"gated": per_rank[1]} if gated else {})}}
                if pdist.active() else {}),
@@ -967,9 +990,13 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                          "algorithmic_bytes_timed": bytes_timed,
                          "avg_kernel_ms": kern_avg_ms, "kernel_ms_timed": kern_total_ms,
                          "launches": len(plan),
-                         "timing": "two HIP events on the launch stream, before the first and "
-                                   "after the last timed launch (none between launches: each "
-                                   "would idle the GPU ~12 us)"},
+                         "timing": ("two HIP events on the launch stream bound to the gate "
+                                    "wave's exit and to an empty mark kernel's start after the "
+                                    "last timed launch (hipExtLaunchKernel; no marker packet)"
+                                    if head is w_gate and bound_marks else
+                                    "two HIP events on the launch stream, before the first and "
+                                    "after the last timed launch (none between launches: each "
+                                    "would idle the GPU ~12 us)")},
         }
         if ceiling is not None:
             ceiling["frac_of_spec"] = ceiling["achieved"] / HBM_PEAK_GBS
@@ -1028,6 +1055,10 @@ def main():
                     help="gated (philox): the window's launches are queued behind a launch gate "
                          "released at t0, so host issue is outside it; the host-issued window is "
                          "measured too and nested as host_issued.  host: host-issued only")
+    ap.add_argument("--marks", default="bound", choices=["bound", "events"],
+                    help="gated window's kernel-span events: bound to the gate wave's exit and to "
+                         "an empty mark kernel after the last launch (no marker packet), or "
+                         "hipEventRecord markers")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
@@ -1082,7 +1113,8 @@ def main():
         del env2
         if rank == 0:
             keep = ("value", "kernel_value", "fixed_overhead_ms", "ms_per_step", "scaling",
-                    "config", "roofline", "steps", "issue", "gate", "host_issued", "per_rank")
+                    "config", "roofline", "steps", "issue", "marks", "gate", "host_issued",
+                    "per_rank")
             out[f"{other}_scaling_line"] = {k: o2[k] for k in keep if k in o2}
     if rank == 0:
         if world == 1 and not args.no_policy:
