@@ -565,14 +565,12 @@ class _Gate:
         self.release()
         stream.synchronize()
 
-    def arm(self, exit_event=None):
-        """Enqueue the gate wave; `exit_event` (a created torch.cuda.Event) is bound to its exit."""
-        import ctypes
+    def arm(self):
+        """Enqueue the gate wave (a new release value)."""
         self.value = (self.value + 1) & 0xFFFFFFFF or 1
         self.blk.status[:2] = 0
-        ev = None if exit_event is None else ctypes.c_void_p(exit_event.cuda_event)
         rc = self.L.fenv_stream_gate(self.blk.dev("flag"), self.value, self.TIMEOUT_US,
-                                     self.blk.dev("status"), ev, self.stream)
+                                     self.blk.dev("status"), self.stream)
         if rc:
             self.flib.check(rc, "fenv_stream_gate")
 
@@ -743,7 +741,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         if trace is not None:
             trace.append((what, time.perf_counter()))
 
-    def region(plan, stat_every, evs=None, release_after=None, release=None, bound=False):
+    def region(plan, stat_every, evs=None, release_after=None, release=None):
         """The timed region's work: the launches of `plan`, stats on the first launch of every
         `stat_every` (a stats launch's reduction is issued after the next launch, so it runs
         on the side stream under that launch), then the wait for the last stats (side stream /
@@ -753,21 +751,14 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         before it takes the timestamp; rocprofv3 kernel trace, profiles/r5_region_trace.txt),
         where a launch after a plain kernel or a timing-free event starts at once.
         `release` (gated window) is called once launch `release_after` and the reductions issued
-        after it are queued, or at the end when that is the last launch.  `bound`: evs[0] is
-        already bound to the gate wave's exit, and evs[1] is bound to the start of an empty
-        mark kernel after the last launch (fenv_stream_mark) -- no marker packet in the window."""
+        after it are queued, or at the end when that is the last launch."""
         n = len(plan)
         for k, L in enumerate(plan):
             launch(k, L, stat=not args.no_stats and k % stat_every == 0,
-                   ev=evs[0] if (evs is not None and k == 0 and not bound) else None)
+                   ev=evs[0] if (evs is not None and k == 0) else None)
             stamp(f"launch {k}")
             if evs is not None and k == n - 1:
-                if bound:
-                    rc = L_abi.fenv_stream_mark(vp(evs[1].cuda_event), abi_stream)
-                    if rc:
-                        flib.check(rc, "fenv_stream_mark")
-                else:
-                    evs[1].record(main_s)
+                evs[1].record(main_s)
             flush(before=k)
             stamp(f"stats before {k}")
             if release is not None and k == release_after and k < n - 1:
@@ -834,9 +825,6 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     gated = (args.issue == "gated" and args.reset_mode == "philox"
              and (not pdist.active() or torch.distributed.get_backend() == "nccl"))
     gate = _Gate(flib, L_abi, dev, main_s) if gated else None
-    # gated window's timing events: bound to the gate wave's exit and to an empty kernel's start
-    # after the last launch (args.marks "bound"), or hipEventRecord markers ("events")
-    bound_marks = gated and args.marks == "bound"
 
     def window(use_gate: bool):
         """--warmup steps, a synchronize (+ barrier), then one timed window of `plan`."""
@@ -862,7 +850,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         w = {}
         if use_gate:
             t_arm = time.perf_counter()
-            gate.arm(evs[0] if bound_marks else None)
+            gate.arm()
             rel = min(len(plan), GATE_PREFIX) - 1
             t0 = None
 
@@ -877,8 +865,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 gate.release()
                 stamp("gate released")
 
-            tot = region(plan, stat_every, evs, release_after=rel, release=release,
-                         bound=bound_marks)
+            tot = region(plan, stat_every, evs, release_after=rel, release=release)
         else:
             t0 = time.perf_counter()
             tot = region(plan, stat_every, evs)
@@ -962,7 +949,6 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
             "issue": "gated" if head is w_gate else "host",
-            "marks": "bound" if head is w_gate and bound_marks else "events",
             **({"gate": {**head["gate"], "release_probe": gate_probe,
                          "prefix_issue_ms": head["prefix_issue_ms"],
                          "release_clock_ns": head["release_clock_ns"]}}
@@ -990,13 +976,9 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                          "algorithmic_bytes_timed": bytes_timed,
                          "avg_kernel_ms": kern_avg_ms, "kernel_ms_timed": kern_total_ms,
                          "launches": len(plan),
-                         "timing": ("two HIP events on the launch stream bound to the gate "
-                                    "wave's exit and to an empty mark kernel's start after the "
-                                    "last timed launch (hipExtLaunchKernel; no marker packet)"
-                                    if head is w_gate and bound_marks else
-                                    "two HIP events on the launch stream, before the first and "
-                                    "after the last timed launch (none between launches: each "
-                                    "would idle the GPU ~12 us)")},
+                         "timing": "two HIP events on the launch stream, before the first and "
+                                   "after the last timed launch (none between launches: each "
+                                   "would idle the GPU ~12 us)"},
         }
         if ceiling is not None:
             ceiling["frac_of_spec"] = ceiling["achieved"] / HBM_PEAK_GBS
@@ -1055,10 +1037,6 @@ def main():
                     help="gated (philox): the window's launches are queued behind a launch gate "
                          "released at t0, so host issue is outside it; the host-issued window is "
                          "measured too and nested as host_issued.  host: host-issued only")
-    ap.add_argument("--marks", default="bound", choices=["bound", "events"],
-                    help="gated window's kernel-span events: bound to the gate wave's exit and to "
-                         "an empty mark kernel after the last launch (no marker packet), or "
-                         "hipEventRecord markers")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
@@ -1113,7 +1091,7 @@ def main():
         del env2
         if rank == 0:
             keep = ("value", "kernel_value", "fixed_overhead_ms", "ms_per_step", "scaling",
-                    "config", "roofline", "steps", "issue", "marks", "gate", "host_issued",
+                    "config", "roofline", "steps", "issue", "gate", "host_issued",
                     "per_rank")
             out[f"{other}_scaling_line"] = {k: o2[k] for k in keep if k in o2}
     if rank == 0:

@@ -38,7 +38,7 @@ extern "C" {
  *   3  + fenv_status, fenv_test_stage_hook, fenv_pinned_pool_bytes, fenv_debug_staging (no
  *        signature changed)
  *   4  + fenv_host_alloc, fenv_host_free (no signature changed)
- *   5  + fenv_stream_gate, fenv_stream_mark (no signature changed) */
+ *   5  + fenv_stream_gate (no signature changed) */
 #define FENV_ABI_VERSION 5
 int fenv_abi_version(void);
 
@@ -180,17 +180,10 @@ int fenv_reduce_partials(const float *partial, int64_t count, double *out, void 
  * fenv_host_alloc block (the host stores the value with a plain write; the kernel polls it with
  * system-scope loads over the bus).  status (device address, may be NULL; 8 bytes) receives
  * status[0] = 1 (released by the flag) or 2 (timed out) and status[1] = the number of polls.
- * exit_event (a hipEvent_t created by the caller, may be NULL) records the wave's stop time from
- * the dispatch's own completion timestamps, with no marker packet between the gate and the next
- * launch.  Use: enqueue a batch of launches behind the gate, then release it, so the host's issue
- * time of the batch is off the device's critical path (bench.py's timed region). */
+ * Use: enqueue a batch of launches behind the gate, then release it, so the host's issue time of
+ * the batch is off the device's critical path (bench.py's timed region). */
 int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, uint32_t *status,
-                     void *exit_event, void *stream);
-/* Timing mark: enqueues an empty one-wave kernel on `stream` whose dispatch start time `event` (a
- * caller-created hipEvent_t) records -- after a kernel on the stream, the moment that kernel
- * retired.  hipEventRecord puts a marker packet in the queue instead, which idles the GPU
- * 11.5-13 us when it sits between two kernels. */
-int fenv_stream_mark(void *event, void *stream);
+                     void *stream);
 
 /* Per-formation statistics the reference logs to wandb (rew [A] may be NULL -> 0), out [F][8] f32:
  *   0 avg_dist_to_goal, 1 ave_dist_to_neighbor, 2 std_dist_to_neighbor (unbiased, NaN when

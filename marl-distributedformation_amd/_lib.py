@@ -45,8 +45,7 @@ SIGNATURES = {
     "fenv_partial_count": (_I64, [_P]),
     "fenv_rollout_kernel": (ctypes.c_char_p, [_P, _I32]),
     "fenv_reduce_partials": (_I32, [_P, _I64, _P, _P]),
-    "fenv_stream_gate": (_I32, [_P, _U32, _I64, _P, _P, _P]),
-    "fenv_stream_mark": (_I32, [_P, _P]),
+    "fenv_stream_gate": (_I32, [_P, _U32, _I64, _P, _P]),
     "fenv_metrics": (_I32, [_P, _P, _P, _P, _P]),
     "fenv_get_state": (_I32, [_P, _P, _P, _P, _P, _P, _P]),
     "fenv_get_state_range": (_I32, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P]),

@@ -897,7 +897,7 @@ int fenv_reduce_partials(const float *partial, int64_t count, double *out, void 
 }
 
 int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, uint32_t *status,
-                     void *exit_event, void *stream) {
+                     void *stream) {
     if (!flag || timeout_us <= 0 || timeout_us > 60000000)
         return fail(FENV_EINVAL, "fenv_stream_gate: NULL flag or timeout_us not in (0, 60 s]");
     int dev = 0, khz = 0;
@@ -905,14 +905,7 @@ int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, u
     FENV_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
     if (khz <= 0) return fail(FENV_EHIP, "fenv_stream_gate: no wall-clock rate");
     const uint64_t ticks = (uint64_t)timeout_us * (uint64_t)khz / 1000u;
-    FENV_HIP(fenvk::launch_stream_gate(flag, value, ticks, status,
-                                       reinterpret_cast<hipEvent_t>(exit_event), as_stream(stream)));
-    return FENV_OK;
-}
-
-int fenv_stream_mark(void *event, void *stream) {
-    if (!event) return fail(FENV_EINVAL, "fenv_stream_mark: NULL event");
-    FENV_HIP(fenvk::launch_stream_mark(reinterpret_cast<hipEvent_t>(event), as_stream(stream)));
+    FENV_HIP(fenvk::launch_stream_gate(flag, value, ticks, status, as_stream(stream)));
     return FENV_OK;
 }
 

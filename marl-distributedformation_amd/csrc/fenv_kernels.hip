@@ -15,7 +15,6 @@
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 
 #include "env_device.h"
 
@@ -921,22 +920,10 @@ __global__ __launch_bounds__(64) void k_stream_gate(const uint32_t *flag, uint32
     }
 }
 
-// exit_ev (may be NULL) is bound to the wave's stop time through the dispatch's own completion
-// timestamps (hipExtLaunchKernel): no marker packet of its own between the gate and the next launch.
 hipError_t launch_stream_gate(const uint32_t *flag, uint32_t value, uint64_t timeout_ticks,
-                              uint32_t *status, hipEvent_t exit_ev, hipStream_t st) {
-    hipExtLaunchKernelGGL(k_stream_gate, dim3(1), dim3(64), 0, st, nullptr, exit_ev, 0u, flag,
-                          value, timeout_ticks, status);
-    return hipGetLastError();
-}
-
-// fenv_stream_mark: an empty wave whose dispatch start time is bound to `ev`.  After a kernel on
-// the same stream it starts as that kernel retires, with no marker packet (a timing marker between
-// two kernels idles the GPU 11.5-13 us, profiles/r5_region_trace.txt).
-__global__ __launch_bounds__(64) void k_stream_mark() {}
-
-hipError_t launch_stream_mark(hipEvent_t ev, hipStream_t st) {
-    hipExtLaunchKernelGGL(k_stream_mark, dim3(1), dim3(64), 0, st, ev, nullptr, 0u);
+                              uint32_t *status, hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_gate, dim3(1), dim3(64), 0, st, flag, value, timeout_ticks,
+                       status);
     return hipGetLastError();
 }
 
