@@ -2,7 +2,8 @@
 # Interleaved A/B of bench.py argument sets on the driver's window (--steps 20 --warmup 5, secondary
 # lines off): for each round, size and variant one bench process; then one summary row per
 # variant and size (value, fixed overhead, kernel_value).  Parameters (env):
-#   VARIANTS  ';'-separated bench argument sets, e.g. "--marks bound;--marks events"
+#   VARIANTS  ';'-separated variants, each bench arguments and/or VAR=value environment settings,
+#             e.g. "--issue gated;--issue host" or "ROC_ACTIVE_WAIT_TIMEOUT=2000;--issue gated"
 #   SIZES     formations per run (default "131072 1048576"); ROUNDS (default 3); TAG (output dir)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -12,8 +13,10 @@ IFS=';' read -ra V <<< "${VARIANTS:?set VARIANTS}"
 for r in $(seq 1 ${ROUNDS:-3}); do
   for F in ${SIZES:-131072 1048576}; do
     for i in "${!V[@]}"; do
-      timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 --formations $F --no-policy \
-        --no-configs --no-cpu-baseline ${V[$i]} > "$O/v${i}_${F}_$r.json" 2> "$O/v${i}_${F}_$r.err" \
+      E=(); A=()
+      for t in ${V[$i]}; do case "$t" in --*) A+=("$t");; *=*) E+=("$t");; *) A+=("$t");; esac; done
+      timeout -k 10 120 env "${E[@]}" python bench.py --gpus 1 --steps 20 --warmup 5 --formations $F \
+        --no-policy --no-configs --no-cpu-baseline "${A[@]}" > "$O/v${i}_${F}_$r.json" 2> "$O/v${i}_${F}_$r.err" \
         || { echo "FAIL variant $i size $F rc=$?"; tail -3 "$O/v${i}_${F}_$r.err"; exit 1; }
     done
   done
