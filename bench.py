@@ -541,6 +541,7 @@ def hbm_ceiling(acts, obs, rew, done, A: int, T: int, D: int, stream, reps: int 
 
 
 GATE_PREFIX = 64  # launches issued behind the launch gate before it is released (bench window)
+ALIGN_MARGIN_NS = 1_000_000  # N > 1: the windows start this long after the ranks agree on when
 
 
 class _Gate:
@@ -848,6 +849,24 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         gc.collect()
         gc.disable()
         w = {}
+        # With a process group, the ranks start their windows at one agreed instant of the node's
+        # monotonic clock (one all-reduce before the window): each rank queues its prefix, then
+        # spins until that instant.  Otherwise a rank whose host issued faster would start early
+        # and then wait, inside its window, for the later ranks' stats all-reduce -- the skew of
+        # the ranks' issue times would add to the max over ranks.
+        start_at = (int(pdist.max_over_ranks(time.monotonic_ns() + ALIGN_MARGIN_NS, dev))
+                    if pdist.active() else None)
+
+        def aligned():
+            """Spin to the agreed start (no-op without a process group); record lateness."""
+            if start_at is None:
+                return
+            now = entry = time.monotonic_ns()
+            w["start_late_us"] = max(0, now - start_at) / 1e3
+            # bounded: ranks on different hosts would not share the clock (bench runs one node)
+            while now < start_at and now - entry < 2 * ALIGN_MARGIN_NS:
+                now = time.monotonic_ns()
+
         if use_gate:
             t_arm = time.perf_counter()
             gate.arm()
@@ -857,6 +876,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             def release():
                 nonlocal t0
                 w["prefix_issue_ms"] = (time.perf_counter() - t_arm) * 1e3
+                aligned()
                 t0 = time.perf_counter()
                 # host clocks of the store, to place it on a rocprofv3 kernel trace's time axis
                 # (tools/gate_latency.py: store -> gate wave exit -> first launch start)
@@ -867,6 +887,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
 
             tot = region(plan, stat_every, evs, release_after=rel, release=release)
         else:
+            aligned()
             t0 = time.perf_counter()
             tot = region(plan, stat_every, evs)
         t_issued = time.perf_counter() - t0
@@ -903,12 +924,14 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     ceiling_small = hbm_ceiling(acts[0], obs, rew, done, A, min(T, 4), D, main_s)
     # per-rank timings of both windows (one all-gather), then the max over ranks
     wins = [w for w in (w_host, w_gate) if w is not None]
-    mine = [x for w in wins for x in (w["elapsed"] * 1e3, w["kern_ms"], w["host_issue_ms"])]
+    mine = [x for w in wins for x in (w["elapsed"] * 1e3, w["kern_ms"], w["host_issue_ms"],
+                                      w.get("start_late_us", 0.0))]
     per = pdist.gather_floats(mine, dev)
     per_rank = []
     for i, w in enumerate(wins):
-        cols = [[r[3 * i + j] for r in per] for j in range(3)]
-        per_rank.append({"elapsed_ms": cols[0], "kernel_ms": cols[1], "host_issue_ms": cols[2]})
+        cols = [[r[4 * i + j] for r in per] for j in range(4)]
+        per_rank.append({"elapsed_ms": cols[0], "kernel_ms": cols[1], "host_issue_ms": cols[2],
+                         "start_late_us": cols[3]})
         w["elapsed_max"] = max(cols[0]) * 1e-3
         w["kern_ms_max"] = max(cols[1])
     elapsed, kern_total_ms, tot = head["elapsed_max"], head["kern_ms_max"], head["tot"]

@@ -55,6 +55,8 @@ def test_bench_region_over_rccl_world1():
     assert set(pr) == {"host", "gated"}
     for w in pr.values():
         assert all(len(v) == 1 for v in w.values())
+        # the window started at the agreed instant (1 ms after the agreement), not late
+        assert 0.0 <= w["start_late_us"][0] < 1000.0
     assert abs(pr["gated"]["elapsed_ms"][0] - rccl["ms_per_step"] * rccl["steps"]) < 1e-6
     assert "per_rank" not in plain
     # the all-reduced stats equal the unreduced ones bit for bit (same seed, same launches)
