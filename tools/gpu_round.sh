@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU call for a round's evidence: GPU tests, the driver's bench command, the default bench,
+# One GPU call for a round's evidence: GPU tests, smoke(), the driver's bench command, the default bench,
 # a rocprofv3 kernel-trace/stats profile of the driver's command, and the two PMC traffic passes.
 # Each GPU step has its own time limit; any failure other than a plain test failure stops it.
 set -u
@@ -16,6 +16,9 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   rc=$?; echo "pytest rc=$rc"; tail -4 "$O/pytest_gpu.log"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || fatal $rc pytest
 fi
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke: ok')" > "$O/smoke.log" 2>&1 \
+  || fatal $? smoke
+echo "smoke ok"
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err" || fatal $? bench_driver
 echo "bench(driver cmd):"; cat "$O/bench_driver.json" | cut -c1-900
 if [ -z "${SKIP_DEFAULT:-}" ]; then
