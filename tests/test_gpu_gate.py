@@ -56,3 +56,26 @@ def test_gate_times_out_without_release(flib, blk):
     blk.flag[0] = 4
     st.synchronize()
     assert blk.status[0] == 1
+
+
+def test_gate_holds_work_ordered_after_it_on_other_streams(flib, blk):
+    """bench.py's window: the side stream's reductions wait on events recorded on the gated
+    stream, so they are held too, and run once the gate is released."""
+    main = torch.cuda.current_stream(DEV)
+    side = torch.cuda.Stream(DEV)
+    y = torch.zeros(4096, device=DEV)
+    mark, done = torch.cuda.Event(), torch.cuda.Event()
+    torch.cuda.synchronize()
+    _arm(flib, blk, 11, 5_000_000)
+    y.fill_(2.0)                                  # on the gated stream
+    mark.record(main)
+    side.wait_event(mark)
+    with torch.cuda.stream(side):
+        y.mul_(3.0)                               # ordered after the gated fill
+    done.record(side)
+    time.sleep(0.03)
+    assert not done.query() and blk.status[0] == 0
+    blk.flag[0] = 11
+    done.synchronize()
+    assert blk.status[0] == 1
+    assert torch.all(y == 6.0).item()
