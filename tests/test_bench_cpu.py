@@ -31,3 +31,23 @@ def test_cpu_share_within_affinity():
     import os
     threads, how = bench.cpu_share()
     assert 1 <= threads <= len(os.sched_getaffinity(0)) and "affinity" in how
+
+
+def test_window_summary_fields():
+    """One window's JSON fields from its max-over-ranks wall and kernel times: value over the
+    wall, kernel_value over the event-timed span, fixed overhead = the difference."""
+    w = {"elapsed_max": 1.0e-3, "kern_ms_max": 0.9, "host_issue_ms": 0.05}
+    s = bench.window_summary(w, total_agents=5_000_000, steps=20)
+    assert abs(s["value"] - 1e11) < 1.0
+    assert abs(s["kernel_value"] - 1e11 / 0.9) < 1.0
+    assert abs(s["ms_per_step"] - 0.05) < 1e-12
+    assert abs(s["fixed_overhead_ms"] - 0.1) < 1e-12
+    assert s["kernel_ms_timed"] == 0.9 and s["host_issue_ms"] == 0.05
+
+
+def test_gate_prefix_and_alignment_constants():
+    """The gated window queues at most GATE_PREFIX launches before its release, and N > 1 windows
+    start ALIGN_MARGIN_NS after the ranks agree."""
+    assert bench.GATE_PREFIX >= 2          # the driver's --steps 20 window is gated whole
+    assert 0 < bench.ALIGN_MARGIN_NS <= 5_000_000
+    assert bench._Gate.TIMEOUT_US <= 60_000_000   # fenv_stream_gate's limit
