@@ -825,7 +825,14 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     # blocks the host until the tensor's producer -- held behind the gate -- has run).
     gated = (args.issue == "gated" and args.reset_mode == "philox"
              and (not pdist.active() or torch.distributed.get_backend() == "nccl"))
-    gate = _Gate(flib, L_abi, dev, main_s) if gated else None
+    gate, gate_error = None, None
+    if gated:
+        try:
+            gate = _Gate(flib, L_abi, dev, main_s)
+        except Exception as ex:  # noqa: BLE001 -- the line then carries the host-issued window
+            gate_error = f"gate setup: {type(ex).__name__}: {ex}"
+        # every rank runs the same windows (each holds collectives)
+        gated = pdist.max_over_ranks(0.0 if gate is not None else 1.0, dev) == 0.0
 
     def window(use_gate: bool):
         """--warmup steps, a synchronize (+ barrier), then one timed window of `plan`."""
@@ -902,8 +909,8 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
         if use_gate:
             w["gate"] = gate.status()
             w["gate"]["prefix_launches"] = min(len(plan), GATE_PREFIX)
-            if w["gate"]["released"] != 1:  # the gate timed out: the window is not a measurement
-                raise RuntimeError(f"launch gate did not release: {w['gate']}")
+            # released != 1: the gate timed out, so this window is not a measurement; the line
+            # then falls back to the host-issued window (below) and says why
         # the closing barrier stays outside the window: max_over_ranks(elapsed) below already takes
         # the slowest rank, and a barrier inside would add a collective's latency to every rank
         if pdist.active():
@@ -915,8 +922,12 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     w_gate = window(True) if gated else None
     if not args.no_gc_freeze:
         gc.unfreeze()
+    if w_gate is not None and pdist.max_over_ranks(
+            0.0 if w_gate["gate"]["released"] == 1 else 1.0, dev) != 0.0:
+        gate_error = f"gate did not release on every rank: {w_gate['gate']}"
+        w_gate = None
     head = w_gate or w_host
-    gate_probe = gate.probe() if gated else None  # after both windows
+    gate_probe = gate.probe() if w_gate is not None else None  # after both windows
     ceiling = hbm_ceiling(acts[0], obs, rew, done, A, T, D, main_s)  # after the timed region
     # the same byte mix over the first 4 planes only: its 0.17 GB of actions stay in the 256 MB
     # Infinity Cache from one k_mix launch to the next, so this is NOT an HBM ceiling -- it shows
@@ -972,12 +983,14 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
             "issue": "gated" if head is w_gate else "host",
+            **({"gate_error": gate_error} if gate_error else {}),
             **({"gate": {**head["gate"], "release_probe": gate_probe,
                          "prefix_issue_ms": head["prefix_issue_ms"],
                          "release_clock_ns": head["release_clock_ns"]}}
                if head is w_gate else {}),
             "host_issued": window_summary(w_host, total_agents, steps),
-            **({"per_rank": {"host": per_rank[0], **({"gated": per_rank[1]} if gated else {})}}
+            **({"per_rank": {"host": per_rank[0],
+                             **({"gated": per_rank[1]} if w_gate is not None else {})}}
                if pdist.active() else {}),
             **({"host_trace_us": head["trace"]} if trace is not None else {}),
             "config": {"workload": workload, "formations": total_formations,
