@@ -62,3 +62,11 @@ def test_bench_region_over_rccl_world1():
     # the all-reduced stats equal the unreduced ones bit for bit (same seed, same launches)
     assert rccl["episode_stats"] == plain["episode_stats"]
     assert rccl["episode_stats"]["agent_dones_sampled_rollout"] >= 0
+
+
+def test_bench_falls_back_to_host_window_when_gate_times_out():
+    """A gate that never sees its release (test hook: the store is skipped; the wave times out
+    after 20 ms) does not take the line down: it carries the host-issued window, labelled."""
+    d = _bench({"FENV_BENCH_GATE_TEST": "no-release"})
+    assert d["issue"] == "host" and "did not release" in d["gate_error"]
+    assert d["value"] == d["host_issued"]["value"] and "gate" not in d
