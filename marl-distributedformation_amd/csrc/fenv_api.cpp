@@ -855,8 +855,8 @@ static int rollout_impl(fenv_t *e, int32_t T, const float *act, const fenvk::Act
         if (event) {
             int rc = e->gen_pending(st);
             // the call's next launch reads the set just staged: its copy runs on the staging
-            // stream, so the launch stream waits for it (tools/job_r5_e.sh caught the missing
-            // wait with the delayed-copy test hook)
+            // stream, so the launch stream waits for it (round 5's staging A/B caught the missing
+            // wait with the delayed-copy test hook; profiles/r5_mt_mode/README.txt)
             if (!rc && k0 + L < T) rc = e->wait_pending(st);
             if (rc) return rc;
         }

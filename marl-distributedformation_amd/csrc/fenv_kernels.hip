@@ -44,7 +44,7 @@ __device__ __forceinline__ float act_u24(uint32_t w) {
 // Register budget: left to the compiler for the Philox kernels (69 VGPRs -> 7 waves/SIMD).  The
 // MT19937 kernel with HBM actions is held to 7 waves/SIMD too: left alone it takes 73 VGPRs (6
 // waves); at 72 it spills only SGPRs (to VGPR lanes) and its rollout runs 1 % faster
-// (tools/job_r5_d.sh, 3 interleaved rounds).  Forcing 64 VGPRs (8 waves) spills VGPRs and runs
+// (profiles/r5_mt_mode/occupancy_ab, 3 interleaved rounds).  Forcing 64 VGPRs (8 waves) spills VGPRs and runs
 // ~12 % slower (archive: tools/env_ab.sh).
 #ifndef FENV_RS_OCC
 #define FENV_RS_OCC __attribute__((amdgpu_waves_per_eu((MODE == 0 && !RA) ? 7 : 1)))
