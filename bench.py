@@ -571,7 +571,7 @@ class _Gate:
     def arm(self):
         """Enqueue the gate wave (a new release value)."""
         self.value = (self.value + 1) & 0xFFFFFFFF or 1
-        self.blk.status[:2] = 0
+        self.blk.status[:4] = 0
         rc = self.L.fenv_stream_gate(self.blk.dev("flag"), self.value, self.TIMEOUT_US,
                                      self.blk.dev("status"), self.stream)
         if rc:
@@ -583,7 +583,9 @@ class _Gate:
         self.blk.flag[0] = self.value
 
     def status(self) -> dict:
-        return {"released": int(self.blk.status[0]), "polls": int(self.blk.status[1])}
+        st = self.blk.status
+        return {"released": int(st[0]), "polls": int(st[1]),
+                "held_us": ((int(st[3]) << 32) | int(st[2])) / 1e3}
 
     def probe(self, reps: int = 21) -> dict:
         us = []

@@ -178,8 +178,10 @@ int fenv_reduce_partials(const float *partial, int64_t count, double *out, void 
  * constant-rate clock have passed -- the wave always exits, so a host that never stores the value
  * costs the stream timeout_us, never a hang.  `flag` is a device address, normally inside a
  * fenv_host_alloc block (the host stores the value with a plain write; the kernel polls it with
- * system-scope loads over the bus).  status (device address, may be NULL; 8 bytes) receives
- * status[0] = 1 (released by the flag) or 2 (timed out) and status[1] = the number of polls.
+ * system-scope loads over the bus).  status (device address, may be NULL; 16 bytes, 8-byte
+ * aligned) receives status[0] = 1 (released by the flag) or 2 (timed out), status[1] = the number
+ * of polls and status[2..3] = the time the wave held the stream, entry to exit, in ns (uint64,
+ * little-endian; from the constant-rate clock), status[0] written last.
  * Use: enqueue a batch of launches behind the gate, then release it, so the host's issue time of
  * the batch is off the device's critical path (bench.py's timed region). */
 int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, uint32_t *status,

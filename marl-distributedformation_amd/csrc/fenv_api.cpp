@@ -905,7 +905,8 @@ int fenv_stream_gate(const uint32_t *flag, uint32_t value, int64_t timeout_us, u
     FENV_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
     if (khz <= 0) return fail(FENV_EHIP, "fenv_stream_gate: no wall-clock rate");
     const uint64_t ticks = (uint64_t)timeout_us * (uint64_t)khz / 1000u;
-    FENV_HIP(fenvk::launch_stream_gate(flag, value, ticks, status, as_stream(stream)));
+    FENV_HIP(fenvk::launch_stream_gate(flag, value, ticks, (uint32_t)khz, status,
+                                       as_stream(stream)));
     return FENV_OK;
 }
 

@@ -136,7 +136,7 @@ hipError_t launch_stage_copy(float *dst, const float *src, int64_t n, int32_t de
 hipError_t launch_reduce_partials(const float *partial, int64_t count, double *out,
                                   hipStream_t st);
 hipError_t launch_stream_gate(const uint32_t *flag, uint32_t value, uint64_t timeout_ticks,
-                              uint32_t *status, hipStream_t st);
+                              uint32_t khz, uint32_t *status, hipStream_t st);
 hipError_t launch_fp_probe(int32_t op, const float *a, const float *b, float *out, int64_t n,
                            hipStream_t st);
 

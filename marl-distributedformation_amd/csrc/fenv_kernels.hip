@@ -898,31 +898,40 @@ hipError_t launch_reduce_partials(const float *partial, int64_t count, double *o
 // host stores `value` into the word at `flag` (coherent, device-mapped host memory: every poll is
 // a system-scope load that crosses the bus, ~1-2 us), or until `timeout_ticks` of the
 // constant-rate wall clock have passed -- an exit every wave reaches, whatever the host does.
-// status[0] = 1 released / 2 timed out, status[1] = polls; written by lane 0 with system-scope
-// stores (vector memory), polls first, so a host that sees status[0] also sees the count.
+// status[0] = 1 released / 2 timed out, status[1] = polls, status[2..3] = the time the wave held
+// the stream (entry to exit, ns, 64-bit); written by lane 0 with system-scope stores (vector
+// memory), status[0] last, so a host that sees it also sees the rest.
 __global__ __launch_bounds__(64) void k_stream_gate(const uint32_t *flag, uint32_t value,
-                                                    uint64_t timeout_ticks, uint32_t *status) {
+                                                    uint64_t timeout_ticks, uint32_t khz,
+                                                    uint32_t *status) {
     const uint64_t t0 = wall_clock64();
+    uint64_t t = t0;
     uint32_t polls = 0, how = 2;
     for (;;) {
         const uint32_t v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         ++polls;
+        t = wall_clock64();
         if (v == value) {
             how = 1;
             break;
         }
-        if (wall_clock64() - t0 > timeout_ticks) break;
+        if (t - t0 > timeout_ticks) break;
         __builtin_amdgcn_s_sleep(8);  // ~0.2 us between polls; a poll itself takes ~1 us
     }
     if (status && threadIdx.x == 0) {
+        const uint64_t held_ns = (t - t0) * 1000000ull / khz;
         __hip_atomic_store(status + 1, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(status + 2, (uint32_t)held_ns, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(status + 3, (uint32_t)(held_ns >> 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(status, how, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 hipError_t launch_stream_gate(const uint32_t *flag, uint32_t value, uint64_t timeout_ticks,
-                              uint32_t *status, hipStream_t st) {
-    hipLaunchKernelGGL(k_stream_gate, dim3(1), dim3(64), 0, st, flag, value, timeout_ticks,
+                              uint32_t khz, uint32_t *status, hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_gate, dim3(1), dim3(64), 0, st, flag, value, timeout_ticks, khz,
                        status);
     return hipGetLastError();
 }

@@ -42,6 +42,8 @@ def test_gate_holds_then_releases(flib, blk):
     blk.flag[0] = 7
     ev.synchronize()
     assert blk.status[0] == 1 and blk.status[1] >= 2
+    held_ms = ((int(blk.status[3]) << 32) | int(blk.status[2])) / 1e6
+    assert 55.0 <= held_ms < 5000.0               # the wave's own clock: held > the 60 ms slept
     assert float(x.sum()) == float(1 << 20)
 
 
@@ -52,6 +54,8 @@ def test_gate_times_out_without_release(flib, blk):
     el = time.perf_counter() - t0
     assert blk.status[0] == 2 and blk.status[1] >= 1
     assert 0.025 < el < 5.0
+    held_ms = ((int(blk.status[3]) << 32) | int(blk.status[2])) / 1e6
+    assert 30.0 <= held_ms < 31.0                 # the timeout, by the wave's clock
     _arm(flib, blk, 4, 5_000_000)                 # re-armed gate is held again, then released
     blk.flag[0] = 4
     st.synchronize()
