@@ -608,41 +608,6 @@ class _Gate:
                         "memory -> the spinning host sees it (two bus crossings)"}
 
 
-class _FenceFreeEvent:
-    """A timing HIP event created with hipEventDisableSystemFence (no system-scope acquire /
-    release at the marker), with torch.cuda.Event's record / elapsed_time.  Bound through the HIP
-    runtime this process already loaded (torch's), found in /proc/self/maps."""
-
-    _hip = None
-
-    def __init__(self):
-        import ctypes
-        if _FenceFreeEvent._hip is None:
-            path = next(ln.split()[-1] for ln in open("/proc/self/maps")
-                        if "libamdhip64.so" in ln)
-            h = ctypes.CDLL(path)
-            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
-            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-            h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
-                                              ctypes.c_void_p]
-            _FenceFreeEvent._hip = h
-        self.ev = ctypes.c_void_p()
-        if self._hip.hipEventCreateWithFlags(ctypes.byref(self.ev), 0x20000000) != 0:
-            raise RuntimeError("hipEventCreateWithFlags(hipEventDisableSystemFence) failed")
-
-    def record(self, stream):
-        import ctypes
-        if self._hip.hipEventRecord(self.ev, ctypes.c_void_p(stream.cuda_stream)) != 0:
-            raise RuntimeError("hipEventRecord failed")
-
-    def elapsed_time(self, other) -> float:
-        import ctypes
-        ms = ctypes.c_float()
-        if self._hip.hipEventElapsedTime(ctypes.byref(ms), self.ev, other.ev) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return ms.value
-
-
 def window_summary(w: dict, total_agents: int, steps: int) -> dict:
     """The JSON fields of one timed window (max over ranks)."""
     return {"value": total_agents * steps / w["elapsed_max"],
@@ -877,8 +842,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
 
     def window(use_gate: bool):
         """--warmup steps, a synchronize (+ barrier), then one timed window of `plan`."""
-        evs = ([_FenceFreeEvent() for _ in range(2)] if use_gate and args.event_fence == "device"
-               else [torch.cuda.Event(enable_timing=True) for _ in range(2)])
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for e in evs:
             e.record(main_s)
         for L in launch_plan(args.warmup, T):
@@ -1115,9 +1079,6 @@ def main():
                     help="gated (philox): the window's launches are queued behind a launch gate "
                          "released at t0, so host issue is outside it; the host-issued window is "
                          "measured too and nested as host_issued.  host: host-issued only")
-    ap.add_argument("--event-fence", default="system", choices=["system", "device"],
-                    help="gated window's timing events: torch's (system-scope fence at the marker) "
-                         "or hipEventDisableSystemFence ones")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
