@@ -173,9 +173,9 @@ def world_rank() -> tuple[int, int]:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    """Replicate ``t`` from rank ``src`` in place (the policy parameters, once at start)."""
-    world, _ = world_rank()
-    if world > 1:
+    """Replicate ``t`` from rank ``src`` in place (the policy parameters, once at start); a real
+    collective whenever a process group is up (world 1 included)."""
+    if active():
         dist.broadcast(t, src)
     return t
 
@@ -197,7 +197,7 @@ def gather_columns(local: torch.Tensor, counts: list[int], out: torch.Tensor | N
     total = sum(counts)
     if out is None:
         out = torch.empty((T, total, C), dtype=local.dtype, device=local.device)
-    if world == 1:
+    if not active():
         out.copy_(local)
         return out
     amax = max(counts)

@@ -70,3 +70,22 @@ def test_bench_falls_back_to_host_window_when_gate_times_out():
     d = _bench({"FENV_BENCH_GATE_TEST": "no-release"})
     assert d["issue"] == "host" and "did not release" in d["gate_error"]
     assert d["value"] == d["host_issued"]["value"] and "gate" not in d
+
+
+def test_ppo_collectives_over_rccl_world1():
+    """The PPO and stats collectives (policy broadcast, the replicated update's sample all-gather,
+    the sharded update's gradient all-reduce, the double-buffered stats all-reduce on a side
+    stream, max_over_ranks, the per-rank gather) run once each on RCCL over device tensors in a
+    world-1 "nccl" group, and are identities there, bit for bit."""
+    env = dict(os.environ)
+    env.update({"FENV_DIST_FORCE": "1", "FENV_DIST_BACKEND": "nccl", "WORLD_SIZE": "1",
+                "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(_port())})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_child.py")], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["backend"] == "nccl" and out["world"] == 1 and out["active"]
+    assert out["broadcast_equal"] and out["gather_equal"] and out["allreduce_equal"]
+    assert out["stats_result"] == [2.0, 2.0]
+    assert out["max_over_ranks"] == 3.25 and out["gather_floats"] == [[1.5, 2.5]]
