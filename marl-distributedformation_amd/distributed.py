@@ -189,7 +189,7 @@ def gather_columns(local: torch.Tensor, counts: list[int], out: torch.Tensor | N
     """All-gather of a [T, A_r, C] tensor whose middle dimension is sharded contiguously over the
     ranks (sizes ``counts``, which may differ by rank) -> [T, sum(counts), C], concatenated in rank
     order along dim 1: exactly the unsharded tensor.  One collective (shards padded to the largest
-    count).  With world size 1 it is a copy."""
+    count) whenever a process group is up (world 1 included); without one it is a copy."""
     world, rank = world_rank()
     T, Ar, C = local.shape
     if Ar != counts[rank]:
