@@ -14,7 +14,10 @@ for r in $(seq 1 ${ROUNDS:-3}); do
   for F in ${SIZES:-131072 1048576}; do
     for i in "${!V[@]}"; do
       E=(); A=()
-      for t in ${V[$i]}; do case "$t" in --*) A+=("$t");; *=*) E+=("$t");; *) A+=("$t");; esac; done
+      for t in ${V[$i]}; do
+        t=${t//RANDOMPORT/$((20000 + RANDOM % 20000))}  # a fresh rendezvous port per process
+        case "$t" in --*) A+=("$t");; *=*) E+=("$t");; *) A+=("$t");; esac
+      done
       timeout -k 10 120 env "${E[@]}" python bench.py --gpus 1 --steps 20 --warmup 5 --formations $F \
         --no-policy --no-configs --no-cpu-baseline "${A[@]}" > "$O/v${i}_${F}_$r.json" 2> "$O/v${i}_${F}_$r.err" \
         || { echo "FAIL variant $i size $F rc=$?"; tail -3 "$O/v${i}_${F}_$r.err"; exit 1; }
