@@ -670,11 +670,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
     reds = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
     main_s = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev)
-    # with an nccl group, the stats all-reduce is one RCCL launch on the side stream (RcclComm):
-    # ProcessGroupNCCL's own stream and its event hops do not fit under an 8-way shard's launch
-    rccl = (pdist.RcclComm(dev) if pdist.active() and args.stats_comm == "rccl"
-            and torch.distributed.get_backend() == "nccl" else None)
-    stats = pdist.StatsReducer(2, dev, stream=side, rccl=rccl)
+    stats = pdist.StatsReducer(2, dev, stream=side)
     mark = [torch.cuda.Event() for _ in range(2)]
     freed = [None, None]  # the reducer event after which partials[s] may be rewritten
     env.reset_tensor()
@@ -973,11 +969,6 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 + ("" if world == 1 else f", {scaling} scaling"))
     traffic, tsrc = load_pmc_traffic(workload if world == 1 else "")
     kname = env.rollout_kernel_name(T)
-    if rccl is not None:
-        torch.cuda.synchronize()
-        rccl.destroy()
-    stats_coll = ("none" if not pdist.active() else
-                  "rccl on the side stream" if rccl is not None else "process group")
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -998,7 +989,6 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             "kernel_value": kernel_value,
             "fixed_overhead_ms": elapsed * 1e3 - kern_total_ms,
             "issue": "gated" if head is w_gate else "host",
-            "stats_collective": stats_coll,
             **({"gate_error": gate_error} if gate_error else {}),
             **({"gate": {**head["gate"], "release_probe": gate_probe,
                          "prefix_issue_ms": head["prefix_issue_ms"],
@@ -1089,9 +1079,6 @@ def main():
                     help="gated (philox): the window's launches are queued behind a launch gate "
                          "released at t0, so host issue is outside it; the host-issued window is "
                          "measured too and nested as host_issued.  host: host-issued only")
-    ap.add_argument("--stats-comm", default="rccl", choices=["rccl", "pg"],
-                    help="nccl group: the stats all-reduce as one RCCL launch on the side stream "
-                         "(RcclComm), or through the process group (its own stream + event hops)")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
@@ -1146,7 +1133,7 @@ def main():
         del env2
         if rank == 0:
             keep = ("value", "kernel_value", "fixed_overhead_ms", "ms_per_step", "scaling",
-                    "config", "roofline", "steps", "issue", "stats_collective", "gate",
+                    "config", "roofline", "steps", "issue", "gate",
                     "host_issued", "per_rank")
             out[f"{other}_scaling_line"] = {k: o2[k] for k in keep if k in o2}
     if rank == 0:

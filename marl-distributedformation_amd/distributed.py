@@ -6,7 +6,6 @@ so env stepping needs no communication.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 
 import torch
@@ -49,77 +48,6 @@ def init_from_env(backend: str | None = None, force: bool | None = None) -> tupl
     return rank, world, local
 
 
-class RcclComm:
-    """The process group's ranks as one RCCL communicator driven through librccl directly (the
-    library torch's "nccl" backend already loaded): a collective is one RCCL launch on the
-    caller's stream.  ProcessGroupNCCL instead runs every collective on its own internal stream,
-    ordered by an event record / wait pair on each side -- queue markers that cost several
-    microseconds each, which a small all-reduce under a 55 us launch cannot hide (bench.py's
-    8-way shard size).  Built collectively (rank 0's unique id is broadcast over the
-    group), so every rank constructs it at the same point."""
-
-    _lib = None
-
-    class _UniqueId(ctypes.Structure):
-        _fields_ = [("internal", ctypes.c_char * 128)]  # NCCL_UNIQUE_ID_BYTES
-
-    def __init__(self, device):
-        if not active() or dist.get_backend() != "nccl":
-            raise RuntimeError("RcclComm needs an initialised 'nccl' process group")
-        L = RcclComm._load()
-        self.device = torch.device(device)
-        rank, world = dist.get_rank(), dist.get_world_size()
-        uid = RcclComm._UniqueId()
-        t = torch.zeros(128, dtype=torch.uint8, device=self.device)
-        if rank == 0:
-            _ok(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-            t.copy_(torch.frombuffer(bytearray(ctypes.string_at(ctypes.byref(uid), 128)),
-                                     dtype=torch.uint8))
-        dist.broadcast(t, 0)
-        ctypes.memmove(ctypes.byref(uid), bytes(t.cpu().numpy()), 128)
-        self.comm = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            _ok(L.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank), "ncclCommInitRank")
-
-    @classmethod
-    def _load(cls):
-        if cls._lib is None:
-            path = next((ln.split()[-1] for ln in open("/proc/self/maps") if "librccl" in ln),
-                        None)
-            if path is None:
-                raise RuntimeError("librccl is not loaded in this process")
-            L = ctypes.CDLL(path)
-            L.ncclGetUniqueId.argtypes = [ctypes.c_void_p]
-            L.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
-                                           RcclComm._UniqueId, ctypes.c_int]
-            L.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                        ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                        ctypes.c_void_p]
-            L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
-            cls._lib = L
-        return cls._lib
-
-    _DTYPES = {torch.float64: 8, torch.float32: 7, torch.int64: 4, torch.int32: 2}
-
-    def all_reduce_(self, v: torch.Tensor, stream) -> None:
-        """In-place SUM all-reduce of contiguous ``v`` as one RCCL launch on ``stream``."""
-        if not v.is_contiguous() or v.dtype not in self._DTYPES or v.device != self.device:
-            raise ValueError("RcclComm.all_reduce_: contiguous f64/f32/i64/i32 on its device")
-        p = ctypes.c_void_p(v.data_ptr())
-        _ok(self._lib.ncclAllReduce(p, p, v.numel(), self._DTYPES[v.dtype], 0, self.comm,
-                                    ctypes.c_void_p(stream.cuda_stream)), "ncclAllReduce")
-
-    def destroy(self) -> None:
-        if self.comm is not None and self.comm.value:
-            self._lib.ncclCommDestroy(self.comm)
-        self.comm = None
-
-
-def _ok(rc: int, what: str) -> None:
-    if rc != 0:
-        raise RuntimeError(f"{what} failed (ncclResult {rc})")
-
-
 class StatsReducer:
     """Stream-overlapped all-reduce of a small stats vector, two submissions in flight.
 
@@ -143,9 +71,8 @@ class StatsReducer:
     ``wait()`` blocks the host until the collective is done, so ``submit`` is synchronous there:
     a gloo rehearsal (tools/scale_rehearsal.sh) does not measure the overlapped stats path."""
 
-    def __init__(self, n: int, device, stream=None, rccl: "RcclComm | None" = None):
+    def __init__(self, n: int, device, stream=None):
         self.device = torch.device(device)
-        self.rccl = rccl  # submissions go straight to RCCL on the stream (no PG stream hops)
         self.work = [None, None]
         self.bufs = [None, None]
         self.k = 0
@@ -186,15 +113,11 @@ class StatsReducer:
             elif stream is None:
                 self.dep.record(torch.cuda.current_stream(self.device))
                 st.wait_event(self.dep)
-            if self.dist and self.rccl is not None:
-                self.rccl.all_reduce_(v, st)
+            with torch.cuda.stream(st):
+                if self.dist:
+                    # stream-ordered: wait() only makes the side stream wait for the collective
+                    dist.all_reduce(v, async_op=True).wait()
                 self.done[s].record(st)
-            else:
-                with torch.cuda.stream(st):
-                    if self.dist:
-                        # stream-ordered: wait() only makes the side stream wait for the collective
-                        dist.all_reduce(v, async_op=True).wait()
-                    self.done[s].record(st)
             self.used[s] = True
         else:
             self.reserve()
