@@ -31,7 +31,7 @@ o, names = sys.argv[1], sys.argv[2].split(";")
 rows = {}
 for f in sorted(glob.glob(o + "/v*_*_*.json")):
     i, F, _ = f.rsplit("/", 1)[1][1:-5].split("_")
-    d = json.load(open(f))
+    d = json.loads([x for x in open(f) if x.startswith("{")][-1])
     rows.setdefault((int(F), int(i)), []).append(d)
 for (F, i), ds in sorted(rows.items()):
     print(f"{F:>8} [{names[i]}] value", " ".join("%.3e" % d["value"] for d in ds),
