@@ -718,11 +718,19 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
             _, s = pending.pop(0)
             issue_stats(s, main_s if last else side)
 
+    stall_us = float(os.environ.get("FENV_BENCH_STALL_US", "0") or 0)
+
     def launch(k, L, stat=False, ev=None):
         """Launch k of a region: one fused rollout of L steps (actions of slot nstat-parity;
         stats if `stat`).  `ev` is recorded on the launch stream right before the kernel (after
         any stream-ordering call)."""
         s = nstat[0] % 2
+        if stall_us and k == 1:
+            # test hook (FENV_BENCH_STALL_US): a host stall of this length right before the
+            # window's second launch is issued, like the 80-250 us ones round 5 saw in HIP calls
+            t = time.perf_counter()
+            while (time.perf_counter() - t) * 1e6 < stall_us:
+                pass
         if stat and freed[s] is not None and not freed[s].query():
             # (a reduction the host already saw complete needs no wait packet in the queue)
             main_s.wait_event(freed[s])

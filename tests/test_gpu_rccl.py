@@ -89,3 +89,19 @@ def test_ppo_collectives_over_rccl_world1():
     assert out["broadcast_equal"] and out["gather_equal"] and out["allreduce_equal"]
     assert out["stats_result"] == [2.0, 2.0]
     assert out["max_over_ranks"] == 3.25 and out["gather_floats"] == [[1.5, 2.5]]
+
+
+def test_gated_window_absorbs_a_host_stall():
+    """What the gate is for: a 300 us host stall injected right before the window's second launch
+    is issued (test hook FENV_BENCH_STALL_US) lands inside the host-issued window -- at the 8-way
+    shard size its first launch runs only ~55 us -- and outside the gated one, where the whole
+    window is queued before t0."""
+    d = _bench({"FENV_BENCH_STALL_US": "300"})
+    assert d["issue"] == "gated"
+    host_ms = d["host_issued"]["ms_per_step"] * d["steps"]
+    gated_ms = d["ms_per_step"] * d["steps"]
+    # host-issued: the GPU idles between the two launches (inside the event-timed span too)
+    assert host_ms > 0.3 and d["host_issued"]["kernel_ms_timed"] > 0.25
+    # gated: the ~0.13 ms of the window without a stall (the two launches back to back)
+    assert gated_ms < 0.25 and d["fixed_overhead_ms"] < 0.1
+    assert d["gate"]["prefix_issue_ms"] > 0.3                # the stall happened, before t0
