@@ -92,16 +92,16 @@ def test_ppo_collectives_over_rccl_world1():
 
 
 def test_gated_window_absorbs_a_host_stall():
-    """What the gate is for: a 300 us host stall injected right before the window's second launch
+    """What the gate is for: a 400 us host stall injected right before the window's second launch
     is issued (test hook FENV_BENCH_STALL_US) lands inside the host-issued window -- at the 8-way
     shard size its first launch runs only ~55 us -- and outside the gated one, where the whole
     window is queued before t0."""
-    d = _bench({"FENV_BENCH_STALL_US": "300"})
+    d = _bench({"FENV_BENCH_STALL_US": "400"})
     assert d["issue"] == "gated"
     host_ms = d["host_issued"]["ms_per_step"] * d["steps"]
     gated_ms = d["ms_per_step"] * d["steps"]
     # host-issued: the GPU idles between the two launches (inside the event-timed span too)
-    assert host_ms > 0.3 and d["host_issued"]["kernel_ms_timed"] > 0.25
+    assert host_ms > 0.4 and d["host_issued"]["kernel_ms_timed"] > 0.35
     # gated: the ~0.13 ms of the window without a stall (the two launches back to back)
-    assert gated_ms < 0.25 and d["fixed_overhead_ms"] < 0.1
-    assert d["gate"]["prefix_issue_ms"] > 0.3                # the stall happened, before t0
+    assert gated_ms < 0.35 and host_ms - gated_ms > 0.25
+    assert d["gate"]["prefix_issue_ms"] > 0.4                # the stall happened, before t0
