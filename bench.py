@@ -669,7 +669,7 @@ def run_config3(args, pkg, rank: int, world: int, dev, total_formations: int, sc
                 for _ in range(2)]
     reds = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
     main_s = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev, priority=-1 if args.side_priority == "high" else 0)
+    side = torch.cuda.Stream(dev)
     stats = pdist.StatsReducer(2, dev, stream=side)
     mark = [torch.cuda.Event() for _ in range(2)]
     freed = [None, None]  # the reducer event after which partials[s] may be rewritten
@@ -1087,8 +1087,6 @@ def main():
                     help="gated (philox): the window's launches are queued behind a launch gate "
                          "released at t0, so host issue is outside it; the host-issued window is "
                          "measured too and nested as host_issued.  host: host-issued only")
-    ap.add_argument("--side-priority", default="normal", choices=["normal", "high"],
-                    help="priority of the side stream the stats reductions run on")
     ap.add_argument("--no-gc-freeze", action="store_true",
                     help="A/B switch: no gc.freeze() before the pre-warm")
     ap.add_argument("--no-stats", action="store_true")
